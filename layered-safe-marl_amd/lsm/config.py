@@ -1,0 +1,137 @@
+"""Physical / reward constants and env arguments of the navigation_graph_safe path.
+
+Mirrors ``multiagent/config.py:3-83`` (same class and attribute names, same
+expressions, so float64 values are bit-identical) and the env-side argparse
+fields the reference's ``make_world`` reads (``scripts/train_mpe.py:73-107``,
+``onpolicy/config.py``; canonical values from ``train.sh:15-30``).
+"""
+from __future__ import annotations
+
+import argparse
+from dataclasses import dataclass, asdict
+
+import numpy as np
+
+
+class AirTaxiConfig:
+    V_MIN = 60 * 0.514444 * 0.001
+    V_MAX = 175 * 0.514444 * 0.001
+    V_NOMINAL = 110 * 0.514444 * 0.001
+    ACCEL_MIN = -0.001
+    ACCEL_MAX = 0.002
+    ANGULAR_RATE_MAX = 0.1
+    MOTION_PRIM_ACCEL_OPTIONS = 5
+    MOTION_PRIM_ANGRATE_OPTIONS = 5
+    CBF_RATE = 3.0
+    ENGAGEMENT_DISTANCE = 1.4
+    ENGAGEMENT_DISTANCE_REFERENCE_SEPARATION_DISTANCE = 2200 * 0.0003048
+    DT = 1.0
+    DISTANCE_TO_GOAL_THRESHOLD = 0.35
+    GOAL_HEADING_THRESHOLD = np.pi / 4
+    GOAL_SPEED_THRESHOLD = 0.03
+    SEPARATION_DISTANCE = 1500 * 0.0003048
+    COORDINATION_RANGE = 3 * 1.60934
+
+
+class DoubleIntegratorConfig:
+    VX_MIN = -0.5
+    VX_MAX = 0.5
+    VY_MIN = -0.5
+    VY_MAX = 0.5
+    V_MIN = 0.1
+    V_NOMINAL = 0.5
+    V_MAX = np.sqrt(VX_MAX ** 2 + VY_MAX ** 2)
+    ACCELX_MIN = -0.5
+    ACCELX_MAX = 0.5
+    ACCELY_MIN = -0.5
+    ACCELY_MAX = 0.5
+    ACCELX_OPTIONS = 5
+    ACCELY_OPTIONS = 5
+    CBF_RATE = 3.0
+    ENGAGEMENT_DISTANCE = 1.0
+    ENGAGEMENT_DISTANCE_REFERENCE_SEPARATION_DISTANCE = 0.5
+    DT = 0.1
+    DISTANCE_TO_GOAL_THRESHOLD = 0.3
+    GOAL_HEADING_THRESHOLD = np.pi / 4
+    GOAL_SPEED_THRESHOLD = 0.15
+    SEPARATION_DISTANCE = 0.5
+    COORDINATION_RANGE = 4
+
+
+class RewardWeightConfig:
+    MIN_REWARD = -40
+    MAX_REWARD = 50
+    GOAL_REACH = 50
+    SAFETY_VIOLATION = -20
+    HJ_VALUE = -2
+    POTENTIAL_CONFLICT = -1
+    DIFF_FROM_FILTERED_ACTION = -1
+
+
+class RewardBinaryConfig:
+    SAFETY_VIOLATION = False
+    HJ_VALUE = False
+    POTENTIAL_CONFLICT = False
+    SEPARATION_DISTANCE_CURRICULUM = False
+    INITIAL_PHASE_USE_SAFETY_FILTER = False
+    DIFF_FROM_FILTERED_ACTION = False
+
+
+ENTITY_SIZE = 0.050          # multiagent/core.py:261
+EPS_HJ = 0.4                 # multiagent/safety_filter.py:235,410
+
+
+@dataclass
+class EnvArgs:
+    """The env-side flags of ``all_args`` that the path reads."""
+    scenario_name: str = "navigation_graph_safe"
+    dynamics_type: str = "double_integrator"
+    num_agents: int = 3
+    num_landmarks: int = 2
+    num_obstacles: int = 0
+    num_walls: int = 0
+    num_scripted_agents: int = 0
+    world_size: float = 4
+    episode_length: int = 250
+    num_env_steps: int = 1000
+    n_rollout_threads: int = 1
+    use_safety_filter: bool = False
+    num_internal_step: int = 1
+    use_masking: bool = True
+    use_dones: bool = False
+    collaborative: bool = False
+    graph_feat_type: str = "relative"
+    discrete_action: bool = True
+    seed: int = 0
+
+    @staticmethod
+    def from_namespace(ns: argparse.Namespace) -> "EnvArgs":
+        kw = {k: getattr(ns, k) for k in EnvArgs.__dataclass_fields__ if hasattr(ns, k)}
+        return EnvArgs(**kw)
+
+    def to_namespace(self) -> argparse.Namespace:
+        return argparse.Namespace(**asdict(self))
+
+    def validate(self):
+        if self.scenario_name not in ("navigation_graph_safe",):
+            raise ValueError("only the navigation_graph_safe training scenario is on the path")
+        if self.num_obstacles != 0 or self.num_walls != 0 or self.num_scripted_agents != 0:
+            raise ValueError("obstacles/walls/scripted agents are not supported by the graph mask "
+                             "(navigation_graph_safe.py:976-989)")
+        if self.dynamics_type not in ("double_integrator", "airtaxi"):
+            raise ValueError("dynamics_type must be 'double_integrator' or 'airtaxi'")
+        if self.graph_feat_type != "relative":
+            raise ValueError("only graph_feat_type='relative' is on the path (train.sh)")
+        if self.num_landmarks < 1:
+            raise ValueError("num_landmarks must be >= 1")
+        if self.num_internal_step != 1:
+            raise ValueError("num_internal_step != 1 is not supported")
+        if not self.discrete_action:
+            raise ValueError("only the Discrete(25) action space is on the path")
+        total = int(self.num_env_steps) // self.episode_length // self.n_rollout_threads
+        if total == 0:
+            raise ValueError("num_env_steps // episode_length // n_rollout_threads == 0: the "
+                             "reference's update_curriculum divides by it (navigation_graph_safe.py:326)")
+        n_lm = self.num_agents * self.num_landmarks
+        if n_lm > 127:
+            raise ValueError("landmark ids are addressed through np.int8 (navigation_graph_safe.py:581)")

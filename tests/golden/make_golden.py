@@ -1,0 +1,192 @@
+#!/usr/bin/env python
+"""Record golden vectors from the REFERENCE ITSELF (run in the build container only).
+
+Imports ``/root/reference`` with the local stubs of its absent third-party
+packages (``oracle/ref_harness.py``), drives ``GraphMPEEnv`` exactly as
+``GraphSubprocVecEnv``'s worker does (``onpolicy/envs/env_wrappers.py:851-874``:
+step, auto-reset on all-done with the episode index, ep_info appended), and
+stores per-step outputs as small ``.npz`` fixtures in this directory.
+
+The reference never travels to the GPU box; the fixtures do.
+
+Usage:  python tests/golden/make_golden.py
+"""
+from __future__ import annotations
+
+import os
+import sys
+import tempfile
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "layered-safe-marl_amd"))
+
+from oracle import ref_harness  # noqa: E402
+from lsm import hj_tables  # noqa: E402  (table *inputs* shared by reference, oracle and kernel)
+
+FULL_STEPS = (0, 1, 2, 3, 4)
+
+
+def policy(state_values, goals, rng, di, eps=0.25):
+    """Scripted goal-seeking policy with epsilon-random actions (indices in [0, 25))."""
+    n = len(state_values)
+    idx = np.zeros(n, dtype=np.int64)
+    for i in range(n):
+        if rng.random() < eps:
+            idx[i] = rng.integers(0, 25)
+            continue
+        s = state_values[i]
+        g = goals[i]
+        if di:
+            acc = 1.2 * (g - s[:2]) - 1.5 * s[2:]
+            q = np.clip(np.round(acc / 0.25), -2, 2).astype(int) + 2
+            idx[i] = q[0] * 5 + q[1]
+        else:
+            ang = np.arctan2(g[1] - s[1], g[0] - s[0])
+            err = (ang - s[2] + np.pi) % (2 * np.pi) - np.pi
+            w = int(np.clip(np.round(err / 0.05), -2, 2)) + 2
+            a = 4 if s[3] < 0.06 else 1
+            idx[i] = w * 5 + a
+    return idx
+
+
+def pack_adj(adj_list):
+    nz = np.stack([np.asarray(a) != 0 for a in adj_list])
+    return np.packbits(nz.reshape(-1))
+
+
+def run_case(name, args, seed, ep, steps, value_stored=None, ttr_stored=None, inject=None,
+             action_seed=0):
+    work = tempfile.mkdtemp(prefix="lsm_ref_")
+    di = args.dynamics_type == "double_integrator"
+    if value_stored is not None or ttr_stored is not None:
+        ref_harness.write_data_files(work, di_table=value_stored if di else None,
+                                     at_table=None if di else value_stored, ttr_table=ttr_stored)
+    env = ref_harness.make_reference_env(args, work, seed)
+    scen = env.reward_callback.__self__
+    world = env.world
+    N = args.num_agents
+    rng = np.random.default_rng(action_seed)
+    rec = {k: [] for k in ("act", "state", "reached", "done", "dones", "rew", "obs", "adj_bits",
+                           "minrel", "sfilt", "decon", "edges_n", "info_num", "ptime")}
+    full = {}
+    resets = []
+
+    def goals():
+        out = []
+        for ag in world.agents:
+            out.append(scen.get_agent_current_goal(ag, world).state.p_pos.copy())
+        return np.array(out)
+
+    r = ref_harness.run_in(work, env.reset, ep)
+    obs, aid, node, adj, epinfo = r
+    resets.append((0, [epinfo[k] for k in EPKEYS]))
+    full["reset0_obs"] = np.array(obs)
+    full["reset0_node"] = np.array(node, dtype=np.float32)
+    full["reset0_adj"] = np.array(adj, dtype=np.float32)
+    full["reset0_state"] = np.array([a.state.values for a in world.agents])
+    full["reset0_lm"] = np.array([[l.state.p_pos[0], l.state.p_pos[1], l.heading, l.speed]
+                                  for l in world.landmarks])
+    full["reset0_edges"] = np.array(world.edge_list)
+    if inject is not None:
+        inject(world, scen)
+        full["inject_state"] = np.array([a.state.values for a in world.agents])
+        full["inject_reached"] = np.array(scen.reached_goal)
+    for t in range(steps):
+        st = np.array([a.state.values for a in world.agents])
+        a_idx = policy(st, goals(), rng, di)
+        onehot = ref_harness.one_hot_actions(a_idx)
+        res = ref_harness.run_in(work, env.step, list(onehot))
+        obs, aid, node, adj, rew, done_n, info = res
+        edges = np.array(world.edge_list)
+        rec["act"].append(a_idx)
+        rec["state"].append(np.array([a.state.values for a in world.agents]))
+        rec["reached"].append(np.array(scen.reached_goal))
+        rec["done"].append(np.array([a.done for a in world.agents]))
+        rec["dones"].append(np.array(done_n))
+        rec["rew"].append(np.array(rew, dtype=np.float64))
+        rec["obs"].append(np.array(obs))
+        rec["adj_bits"].append(pack_adj(adj))
+        rec["minrel"].append(np.array([a.min_relative_distance for a in world.agents]))
+        rec["sfilt"].append(np.array([a.safety_filtered for a in world.agents]))
+        rec["decon"].append(np.array([a.deconflicting_agent_index for a in world.agents]))
+        rec["edges_n"].append(edges.shape[1])
+        rec["info_num"].append(np.array([[inf[k] for k in INFOKEYS] for inf in info], dtype=np.float64))
+        rec["ptime"].append(np.array([a.state.p_dist for a in world.agents]))
+        changed = t > 0 and not np.array_equal(rec["done"][-1], rec["done"][-2])
+        if t in FULL_STEPS or t % 50 == 0 or changed:
+            full["t%03d_node" % t] = np.array(node, dtype=np.float32)
+            full["t%03d_adj" % t] = np.array(adj, dtype=np.float32)
+            full["t%03d_edges" % t] = edges
+        if np.all(done_n):
+            r = ref_harness.run_in(work, env.reset, ep)
+            obs, aid, node, adj, epinfo = r
+            resets.append((t + 1, [epinfo[k] for k in EPKEYS]))
+            full["t%03d_reset_obs" % t] = np.array(obs)
+            full["t%03d_reset_state" % t] = np.array([a.state.values for a in world.agents])
+            full["t%03d_reset_lm" % t] = np.array(
+                [[l.state.p_pos[0], l.state.p_pos[1], l.heading, l.speed] for l in world.landmarks])
+            full["t%03d_reset_node" % t] = np.array(node, dtype=np.float32)
+            full["t%03d_reset_adj" % t] = np.array(adj, dtype=np.float32)
+    out = {k: np.array(v) for k, v in rec.items()}
+    out.update(full)
+    out["resets_t"] = np.array([r[0] for r in resets])
+    out["resets_info"] = np.array([r[1] for r in resets], dtype=np.float64)
+    meta = dict(vars(args)); meta.update(name=name, env_seed=seed, ep=ep, steps=steps)
+    out["meta"] = np.array(repr(meta))
+    path = os.path.join(HERE, name + ".npz")
+    np.savez_compressed(path, **out)
+    print("wrote", path, os.path.getsize(path) // 1024, "KB;",
+          "done agents at end:", int(out["done"][-1].sum()), "resets:", len(resets) - 1,
+          "filtered steps:", int(out["sfilt"].sum()))
+    return path
+
+
+EPKEYS = ("travel_time_mean", "travel_distance_mean", "done_percentage", "num_reached_goal_mean",
+          "conflict_percentage", "min_distance_mean", "min_distance_min", "multiple_engagement_percentage")
+INFOKEYS = ("individual_reward", "min_relative_distance", "Dist_to_goal", "Time_req_to_goal",
+            "Num_agent_collisions", "Distance_mean", "Distance_variance", "Dists_traveled",
+            "Time_mean", "Time_stddev", "Min_time_to_goal", "Safety filtered", "Safety violated")
+
+
+def inject_goal_arrival(world, scen):
+    """Finding 4 fixture: put agent 1 on its last goal (reached_goal = L-1) at goal speed/heading."""
+    L = scen.num_landmark_per_agent
+    N = scen.num_agents
+    scen.reached_goal[1] = L - 1
+    g = world.landmarks[(L - 1) * N + 1]
+    a = world.agents[1]
+    a.state.p_pos = g.state.p_pos.copy()
+    sp = g.speed
+    a.state.p_vel = np.array([sp * np.cos(g.heading), sp * np.sin(g.heading)])
+    world.calculate_distances()
+
+
+def main():
+    if not ref_harness.reference_available():
+        raise SystemExit("reference not available here")
+    A = ref_harness.default_args
+    di_small = hj_tables.synthetic_di_stored((31, 31, 21, 21))
+    at_small = hj_tables.synthetic_airtaxi_stored((25, 25, 24, 7, 7))
+    ttr_small = hj_tables.synthetic_ttr((25, 25, 24, 7))
+    run_case("di_n3_off_ep0", A(num_agents=3, num_env_steps=250 * 4), seed=0, ep=0, steps=400)
+    run_case("di_n8_off_ep2", A(num_agents=8, num_env_steps=250 * 4), seed=1, ep=2, steps=300)
+    run_case("di_n8_on_ep4", A(num_agents=8, num_env_steps=250 * 4, use_safety_filter=True),
+             seed=7, ep=4, steps=300, value_stored=di_small, action_seed=3)
+    run_case("di_n3_on_ep0", A(num_agents=3, num_env_steps=250 * 4, use_safety_filter=True),
+             seed=11, ep=0, steps=60, value_stored=di_small, action_seed=4)
+    run_case("di_n4_inject", A(num_agents=4, num_env_steps=250 * 4), seed=5, ep=4, steps=3,
+             inject=inject_goal_arrival, action_seed=5)
+    run_case("at_n4_on_ep4", A(num_agents=4, num_env_steps=350 * 4, dynamics_type="airtaxi",
+                               world_size=6, episode_length=350, use_safety_filter=True),
+             seed=3, ep=4, steps=200, value_stored=at_small, ttr_stored=ttr_small, action_seed=6)
+    run_case("at_n3_off_ep1", A(num_agents=3, num_env_steps=350 * 4, dynamics_type="airtaxi",
+                                world_size=6, episode_length=350), seed=2, ep=1, steps=120,
+             ttr_stored=ttr_small, action_seed=7)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,59 @@
+"""Shared helpers: load a golden fixture and replay it through an env implementation.
+
+Used by the CPU oracle test (oracle vs reference fixtures) and the GPU parity
+test (HIP path vs the same fixtures). Fixtures come from
+``tests/golden/make_golden.py`` (the reference itself, stub-imported).
+"""
+from __future__ import annotations
+
+import ast
+import glob
+import os
+
+import numpy as np
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+EPKEYS = ("travel_time_mean", "travel_distance_mean", "done_percentage", "num_reached_goal_mean",
+          "conflict_percentage", "min_distance_mean", "min_distance_min", "multiple_engagement_percentage")
+INFOKEYS = ("individual_reward", "min_relative_distance", "Dist_to_goal", "Time_req_to_goal",
+            "Num_agent_collisions", "Distance_mean", "Distance_variance", "Dists_traveled",
+            "Time_mean", "Time_stddev", "Min_time_to_goal", "Safety filtered", "Safety violated")
+
+
+def fixture_names():
+    return sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, "*.npz")))
+
+
+def load(name):
+    z = np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False)
+    meta = ast.literal_eval(str(z["meta"]))
+    return z, meta
+
+
+def tables_for(meta):
+    """Rebuild the (small) synthetic tables the fixture was recorded with."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(GOLDEN), "..", "layered-safe-marl_amd"))
+    from lsm import hj_tables
+    di = meta["dynamics_type"] == "double_integrator"
+    vt = tt = None
+    if meta["use_safety_filter"]:
+        st = hj_tables.synthetic_di_stored((31, 31, 21, 21)) if di else \
+            hj_tables.synthetic_airtaxi_stored((25, 25, 24, 7, 7))
+        vt = hj_tables.value_table_from_stored(st, st["separation_distance"])
+    if not di:
+        tt = hj_tables.ttr_table_from_stored(hj_tables.synthetic_ttr((25, 25, 24, 7)))
+    return vt, tt
+
+
+def table_dict(t):
+    if t is None:
+        return None
+    return dict(lo=t.lo, hi=t.hi, shape=t.shape, periodic=t.periodic, values_hj=t.values_hj,
+                grads_hj=t.grads_hj, separation_distance=t.separation_distance,
+                values=t.values_hj, ttr_max=t.ttr_max)
+
+
+def adj_bits(adj):
+    return np.packbits((np.asarray(adj) != 0).reshape(-1))

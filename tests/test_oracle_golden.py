@@ -1,0 +1,120 @@
+"""Pin the CPU oracle against golden vectors recorded from the reference itself.
+
+Every fixture in tests/golden/ was produced by tests/golden/make_golden.py from
+the stub-imported reference. The oracle (oracle/lsm_oracle.py, integrator
+'rk45' = the reference's own solve_ivp call) must reproduce them BIT-EXACTLY:
+states, reached-goal counters, done masks, rewards, observations, adjacency
+nonzero pattern, edge lists, node features / adjacency values at the recorded
+steps, safety-filter flags and deconflicting indices, info fields, and the
+episode summaries returned at each reset.
+"""
+import numpy as np
+import pytest
+
+from golden_replay import EPKEYS, INFOKEYS, adj_bits, fixture_names, load, table_dict, tables_for
+from oracle.hj_grid import Grid
+from oracle.lsm_oracle import OracleEnv, closed_form_step
+
+NAMES = fixture_names()
+
+
+def _replay(name, integrator="rk45"):
+    z, meta = load(name)
+    vt, tt = tables_for(meta)
+    env = OracleEnv(meta, meta["env_seed"], table_dict(vt), table_dict(tt), integrator=integrator)
+    ep = meta["ep"]
+    out = env.reset(ep)
+    return z, meta, env, out
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_oracle_matches_reference(name):
+    z, meta, env, (obs, aid, node, adj, info) = _replay(name)
+    np.testing.assert_array_equal(np.array(obs), z["reset0_obs"])
+    np.testing.assert_array_equal(np.array(node, dtype=np.float32), z["reset0_node"])
+    np.testing.assert_array_equal(np.array(adj, dtype=np.float32), z["reset0_adj"])
+    np.testing.assert_array_equal(env.s, z["reset0_state"])
+    np.testing.assert_array_equal(env.edge_list, z["reset0_edges"])
+    np.testing.assert_array_equal([info[k] for k in EPKEYS], z["resets_info"][0])
+    if "inject_state" in z.files:
+        env.s[:] = z["inject_state"]
+        env.reached_goal[:] = z["inject_reached"]
+        env.calculate_distances()
+    n_reset = 1
+    for t in range(meta["steps"]):
+        obs, aid, node, adj, rew, dones, infos = env.step(z["act"][t])
+        ctx = "%s step %d" % (name, t)
+        np.testing.assert_array_equal(env.s, z["state"][t], err_msg=ctx)
+        np.testing.assert_array_equal(env.reached_goal, z["reached"][t], err_msg=ctx)
+        np.testing.assert_array_equal(env.done, z["done"][t], err_msg=ctx)
+        np.testing.assert_array_equal(dones, z["dones"][t], err_msg=ctx)
+        np.testing.assert_array_equal(np.array(rew, dtype=np.float64), z["rew"][t], err_msg=ctx)
+        np.testing.assert_array_equal(np.array(obs), z["obs"][t], err_msg=ctx)
+        np.testing.assert_array_equal(adj_bits(adj), z["adj_bits"][t], err_msg=ctx)
+        np.testing.assert_array_equal(env.min_rel_dist, z["minrel"][t], err_msg=ctx)
+        np.testing.assert_array_equal(env.safety_filtered, z["sfilt"][t], err_msg=ctx)
+        np.testing.assert_array_equal(env.deconflicting, z["decon"][t], err_msg=ctx)
+        assert env.edge_list.shape[1] == z["edges_n"][t], ctx
+        np.testing.assert_array_equal(
+            np.array([[inf[k] for k in INFOKEYS] for inf in infos], dtype=np.float64), z["info_num"][t],
+            err_msg=ctx)
+        np.testing.assert_array_equal(env.p_dist, z["ptime"][t], err_msg=ctx)
+        key = "t%03d_node" % t
+        if key in z.files:
+            np.testing.assert_array_equal(np.array(node, dtype=np.float32), z[key], err_msg=ctx)
+            np.testing.assert_array_equal(np.array(adj, dtype=np.float32), z["t%03d_adj" % t], err_msg=ctx)
+            np.testing.assert_array_equal(env.edge_list, z["t%03d_edges" % t], err_msg=ctx)
+        if np.all(dones):
+            obs, aid, node, adj, info = env.reset(meta["ep"])
+            assert z["resets_t"][n_reset] == t + 1
+            np.testing.assert_array_equal([info[k] for k in EPKEYS], z["resets_info"][n_reset], err_msg=ctx)
+            np.testing.assert_array_equal(env.s, z["t%03d_reset_state" % t], err_msg=ctx)
+            np.testing.assert_array_equal(np.array(obs), z["t%03d_reset_obs" % t], err_msg=ctx)
+            np.testing.assert_array_equal(np.array(node, dtype=np.float32), z["t%03d_reset_node" % t])
+            np.testing.assert_array_equal(np.array(adj, dtype=np.float32), z["t%03d_reset_adj" % t])
+            n_reset += 1
+    assert n_reset == len(z["resets_t"])
+
+
+@pytest.mark.parametrize("name", [n for n in NAMES if n.startswith("di_n8")])
+def test_closed_form_matches_rk45(name):
+    """The kernel's closed-form integrator stays within 1e-12 of the reference RK45."""
+    z, meta = load(name)
+    rng = np.random.default_rng(0)
+    for t in range(0, meta["steps"], 7):
+        for s in z["state"][t]:
+            a = rng.choice([-0.5, -0.25, 0.0, 0.25, 0.5], size=2)
+            from scipy.integrate import solve_ivp
+            sol = solve_ivp(lambda tt, y: np.array([y[2], y[3], a[0], a[1]]), [0, 0.1], s, method="RK45")
+            np.testing.assert_allclose(closed_form_step(s, a, 0.1, True), sol.y[:, -1], rtol=0, atol=1e-12)
+
+
+def test_closed_form_airtaxi_accuracy():
+    """Airtaxi closed form vs a tight DOP853 solve (reference RK45 is within 1e-12 of it)."""
+    from scipy.integrate import solve_ivp
+    rng = np.random.default_rng(1)
+    for _ in range(200):
+        s = np.array([rng.uniform(-3, 3), rng.uniform(-3, 3), rng.uniform(-4, 4), rng.uniform(0.03, 0.09)])
+        a = np.array([rng.choice(np.linspace(-0.1, 0.1, 5)), rng.choice(np.linspace(-0.001, 0.002, 5))])
+        ode = lambda t, y: np.array([y[3] * np.cos(y[2]), y[3] * np.sin(y[2]), a[0], a[1]])
+        ref = solve_ivp(ode, [0, 1.0], s, method="DOP853", rtol=1e-13, atol=1e-15).y[:, -1]
+        np.testing.assert_allclose(closed_form_step(s, a, 1.0, False), ref, rtol=0, atol=1e-11)
+
+
+def test_grid_semantics_periodic_and_domain():
+    g = Grid([-1.0, -np.pi], [1.0, np.pi], (5, 8), periodic_dims=(1,))
+    vals = np.arange(40, dtype=np.float32).reshape(5, 8)
+    assert np.isnan(g.interpolate(vals, [1.0001, 0.0]))
+    assert not np.isnan(g.interpolate(vals, [1.0, 0.0]))
+    v1 = g.interpolate(vals, [0.0, 3 * np.pi - 0.1])
+    v2 = g.interpolate(vals, [0.0, np.pi - 0.1])
+    assert abs(float(v1) - float(v2)) < 1e-4
+
+
+def test_product_grads_equal_oracle_grads():
+    import sys
+    from lsm import hj_tables
+    st = hj_tables.synthetic_airtaxi_stored((9, 9, 8, 5, 5))
+    t = hj_tables.value_table_from_stored(st, st["separation_distance"])
+    g = Grid(t.lo, t.hi, t.shape, t.periodic)
+    np.testing.assert_array_equal(g.grad_values(t.values_hj), t.grads_hj)
