@@ -1,0 +1,135 @@
+/*
+ * lsm_rollout.h -- C ABI of the MI355X-native navigation_graph_safe rollout.
+ *
+ * One handle = one device-resident batch of `num_envs` environments (one GPU
+ * process owns one handle; envs shard across GPUs by `env_offset`).  Every
+ * entry point replaces one piece of the reference's vec-env surface:
+ *
+ *   lsm_create/destroy   GraphSubprocVecEnv.__init__/close
+ *                        (onpolicy/envs/env_wrappers.py:951-969, 1014-1024) and the
+ *                        per-env GraphMPEEnv(args) + env.seed(seed + 1000*rank)
+ *                        (multiagent/MPE_env.py:56-84, scripts/train_mpe.py:23-45)
+ *   lsm_set_value_table  HjDataHandle.__init__ (multiagent/safety_filter.py:154-168)
+ *   lsm_set_ttr_table    SafeAamScenario.make_world TTR load (navigation_graph_safe.py:128-138)
+ *   lsm_bind_output      the arrays returned by step/reset (env_wrappers.py:988-1005);
+ *                        caller-owned device buffers (e.g. torch tensors)
+ *   lsm_reset            GraphSubprocVecEnv.reset(num_current_episode) -> env.reset()
+ *                        (env_wrappers.py:998-1005, multiagent/environment.py:1046-1074)
+ *   lsm_step             GraphSubprocVecEnv.step(actions, num_current_episode)
+ *                        (env_wrappers.py:103-110, 851-874, 983-996) ->
+ *                        MultiAgentGraphEnv.step (environment.py:963-1042) incl. the
+ *                        worker's auto-reset on np.all(done) (env_wrappers.py:866-871)
+ *   lsm_last_error       exception text (Python wrapper raises RuntimeError)
+ *
+ * All pointers passed to lsm_step / lsm_bind_output are DEVICE pointers.
+ * Calls are stream-ordered and asynchronous; a handle is not thread-safe.
+ * Return value: 0 on success, nonzero error code (see lsm_last_error).
+ */
+#ifndef LSM_ROLLOUT_H
+#define LSM_ROLLOUT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct lsm_env lsm_env;
+
+enum { LSM_DOUBLE_INTEGRATOR = 0, LSM_AIRTAXI = 1 };
+enum { LSM_ACTIONS_INDEX_I32 = 0, LSM_ACTIONS_ONEHOT_F32 = 1, LSM_ACTIONS_ONEHOT_F64 = 2 };
+
+/* Output slots (caller-owned device buffers; shapes in elements). */
+enum {
+  LSM_OUT_OBS = 0,        /* float32 [n][N][OBS]   OBS = 7 (DI) / 6 (airtaxi)       */
+  LSM_OUT_NODE_OBS = 1,   /* float32 [n][N][E][F]  F = 10 (DI) / 11 (airtaxi)       */
+  LSM_OUT_ADJ = 2,        /* float32 [n][N][E][E]                                   */
+  LSM_OUT_REWARD = 3,     /* float32 [n][N]                                         */
+  LSM_OUT_DONE = 4,       /* uint8   [n][N]                                         */
+  LSM_OUT_RESET_FLAG = 5, /* uint8   [n]      env auto-reset during the last step   */
+  LSM_OUT_EP_INFO = 6,    /* float64 [n][8]   episode summary returned by last reset */
+  LSM_OUT_INFO = 7,       /* float64 [n][N][LSM_INFO_FIELDS] info_callback numbers   */
+  LSM_OUT_EDGES = 8,      /* uint8   [n][E][E] update_graph() connectivity (optional)*/
+  LSM_OUT_STATE = 9,      /* float64 [n][N][4] agent state after the last call      */
+  LSM_NUM_OUT = 10
+};
+
+/* Per-agent info fields (navigation_graph_safe.py:386-450 + environment.py:1025). */
+enum {
+  LSM_INFO_INDIVIDUAL_REWARD = 0, LSM_INFO_MIN_RELATIVE_DISTANCE, LSM_INFO_DIST_TO_GOAL,
+  LSM_INFO_TIME_REQ_TO_GOAL, LSM_INFO_NUM_AGENT_COLLISIONS, LSM_INFO_DISTANCE_MEAN,
+  LSM_INFO_DISTANCE_VARIANCE, LSM_INFO_DISTS_TRAVELED, LSM_INFO_TIME_MEAN, LSM_INFO_TIME_STDDEV,
+  LSM_INFO_MIN_TIME_TO_GOAL, LSM_INFO_SAFETY_FILTERED, LSM_INFO_SAFETY_VIOLATED,
+  LSM_INFO_DECONFLICTING_INDEX, LSM_INFO_ACTION_DIFF, LSM_INFO_REACHED_GOAL,
+  LSM_INFO_FIELDS
+};
+
+typedef struct lsm_config {
+  int32_t dynamics;          /* LSM_DOUBLE_INTEGRATOR / LSM_AIRTAXI                    */
+  int32_t num_envs;          /* envs in this handle (this GPU's shard)                */
+  int32_t num_agents;        /* N                                                      */
+  int32_t num_landmarks;     /* L (per agent)                                          */
+  int32_t episode_length;    /* world_length                                           */
+  int32_t use_safety_filter; /* args.use_safety_filter                                 */
+  int32_t use_masking;       /* args.use_masking                                       */
+  int32_t auto_reset;        /* 1: GraphSubprocVecEnv worker semantics, 0: Dummy       */
+  int32_t emit_edges;        /* 1: fill LSM_OUT_EDGES at the start of each step        */
+  int32_t reserved0;
+  double world_size;         /* args.world_size                                        */
+  int64_t seed;              /* env k (global index env_offset + k) seeded seed+1000*k */
+  int64_t env_offset;
+} lsm_config;
+
+/* Curriculum block for one reset call (navigation_graph_safe.py:324-366), computed by the
+ * host with the reference's own float64 expressions. */
+typedef struct lsm_curriculum {
+  double curriculum_ratio;   /* clip(ep / num_total_episode, 0, 1)                     */
+  double sloped;             /* get_effective_curriculum_ratio_sloped()                */
+  double stair;              /* get_effective_curriculum_ratio_stair()                 */
+  double ratio_airtaxi;      /* sloped(0.25, 0.75), or 1 when use_safety_filter        */
+  double ratio_scenario;     /* 1 when use_safety_filter else sloped (random_scenario) */
+  double goal_heading_error_thresh;
+  double goal_speed_error_thresh;
+  double min_dist_thresh;
+  double separation_distance;
+  double engagement_distance;
+  double world_use_safety_filter; /* 0/1 */
+  double reserved;
+} lsm_curriculum;
+
+int lsm_create(const lsm_config* cfg, lsm_env** out);
+void lsm_destroy(lsm_env* env);
+const char* lsm_last_error(const lsm_env* env);
+
+/* values: float32 [prod(shape)] (values_hj, already negated/shifted); grads: float32
+ * [prod(shape)][gwidth] with gwidth = 4 (ndim <= 4) or 8 (ndim == 5); periodic: 0/1 per dim. */
+int lsm_set_value_table(lsm_env* env, int32_t ndim, const double* lo, const double* hi,
+                        const int32_t* shape, const int32_t* periodic,
+                        const float* values_host, const float* grads_host);
+int lsm_set_ttr_table(lsm_env* env, int32_t ndim, const double* lo, const double* hi,
+                      const int32_t* shape, const int32_t* periodic,
+                      const float* values_host, double ttr_max);
+
+int lsm_bind_output(lsm_env* env, int32_t slot, void* device_ptr, size_t bytes);
+size_t lsm_output_bytes(const lsm_env* env, int32_t slot);
+
+int lsm_reset(lsm_env* env, const lsm_curriculum* cur, void* hip_stream);
+int lsm_step(lsm_env* env, const void* actions_device, int32_t action_kind,
+             const lsm_curriculum* cur_for_auto_reset, void* hip_stream);
+
+/* Shape helpers. */
+int32_t lsm_num_entities(const lsm_env* env);   /* E = N * (1 + L) */
+int32_t lsm_node_features(const lsm_env* env);  /* F */
+int32_t lsm_obs_dim(const lsm_env* env);        /* OBS */
+
+/* Host-side entry points of the SAME scenario-generation / RNG code the reset kernel runs
+ * (no GPU needed): used by CPU tests against numpy's legacy RandomState. */
+int lsm_host_mt_uniforms(uint32_t seed, int32_t count, double lo, double hi, double* out);
+int lsm_host_scenario(const lsm_config* cfg, const lsm_curriculum* cur, uint32_t seed,
+                      double* agent_state /* [N][4] */, double* landmarks /* [NL][4] */);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

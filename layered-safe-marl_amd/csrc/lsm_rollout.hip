@@ -1,0 +1,1587 @@
+// lsm_rollout.hip -- MI355X (gfx950) kernels + C ABI for the navigation_graph_safe rollout.
+//
+// One 64-lane wavefront (one workgroup) per environment. Everything an env needs for a
+// step -- agent states, landmarks, the E x E distance table, pairwise filter scratch and
+// an output staging tile -- lives in that wave's LDS; state arrays in HBM are env-major
+// SoA so a wave's loads/stores of its env are contiguous. One launch does the whole
+// MultiAgentGraphEnv.step (multiagent/environment.py:963-1042) including the worker's
+// auto-reset (onpolicy/envs/env_wrappers.py:866-871):
+//
+//   1. update_graph() edge mask from the state at step start    (navigation_graph_safe.py:996-1015)
+//   2. decode Discrete(25) actions                               (environment.py:386-410)
+//   3. pairwise HJ safety filter, lanes = (ego, other) pairs     (core.py:648-677, safety_filter.py)
+//   4. integrate (closed form), speed clamp, travel distance     (core.py:118-131,199-210)
+//   5. E x E distances in LDS, min relative distance             (core.py:514-543,696-709)
+//   6. obs / reward / goal & done update per agent               (navigation_graph_safe.py:606-875)
+//   7. per-ego node features + masked adjacency with the reference's sequential
+//      snapshot rule (ego i sees agents j <= i after their reward update)  (:932-994)
+//   8. episode statistics, info_callback numbers, done flags      (environment.py:1004-1029)
+//   9. if all agents done: device reset with draw-exact numpy MT19937 replay (:264-366,1199-1367)
+//
+// Numerics: float64 state and decisions, -ffp-contract=off plus explicit fma() only where
+// numpy/OpenBLAS fuses (lsm_numeric.h); HJ grid interpolation in float32 like the
+// reference's JAX (oracle/hj_grid.py defines the semantics). No MFMA: nothing here is a
+// dense contraction; the kernel is bound by HBM writes of the dense per-ego outputs.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/lsm_rollout.h"
+#include "lsm_numeric.h"
+#include "lsm_scenario.h"
+
+namespace lsm {
+
+constexpr int WAVE = 64;
+constexpr int MAXN = 32;        // agents per env supported by the one-wave kernel
+constexpr int MAXE = 64;        // entities per env (N * (1 + L))
+constexpr int MT_WORDS = MT_N + 1;  // key[624] + pos
+constexpr int NCUR = 12;
+constexpr int NSTAT = 6;        // travel_length, travel_distance, done, conflict, min_distance, multiple
+constexpr int NWINFO = 4;       // times_required, dists_to_goal, dist_left_to_goal, num_agent_collisions
+
+struct TableDev {
+  const float* values;
+  const float4* grads;
+  int ndim;
+  int n[5];
+  int stride[5];
+  float lo[5];
+  float sp[5];
+  int periodic[5];
+  int gw;  // float4 per node in grads (1 for <= 4 dims, 2 for 5 dims)
+};
+
+struct StateDev {
+  double* st;        // [n][4][N]
+  double* pdist;     // [n][N]
+  uint8_t* done;     // [n][N]
+  int32_t* reached;  // [n][N]
+  double* lm;        // [n][4][NL]
+  double* gmt;       // [n][N] goal_min_time
+  int32_t* step;     // [n] env.current_step (== world.current_time_step)
+  double* cur;       // [n][NCUR]
+  double* stats;     // [n][NSTAT][N]
+  double* prev;      // [n][8]
+  double* winfo;     // [n][NWINFO][N]
+  uint8_t* sfilt;    // [n][N]  agent.safety_filtered
+  int32_t* decon;    // [n][N]  agent.deconflicting_agent_index
+  double* minrel;    // [n][N]  agent.min_relative_distance
+  double* adiff;     // [n][N]  agent.action_diff
+  uint32_t* mt;      // [n][MT_WORDS]
+};
+
+struct OutDev {
+  float* obs;
+  float* node;
+  float* adj;
+  float* rew;
+  uint8_t* dones;
+  uint8_t* reset_flag;
+  double* ep_info;
+  double* info;
+  uint8_t* edges;
+  double* state;
+};
+
+struct KParams {
+  int n_envs, N, L, NL, E, F, OBS, dyn, episode_length, use_masking, use_filter_arg, auto_reset,
+      emit_edges, action_kind, mode;  // mode 0 = step, 1 = reset all
+  double dt, world_size, coord_range, world_eng, sep_target, max_speed, min_speed, gs_min, gs_max;
+  double act0[5], act1[5];
+  double mag_c[50], mag_s[50];
+  double cos_pi6, two_pi, pi;
+  double di_thr_xmax, di_thr_xmin, di_thr_ymax, di_thr_ymin, di_axmax, di_axmin, di_aymax, di_aymin;
+  double at_vmax, at_vmin, at_amax, at_amin, at_wmax, at_thr_amax, at_thr_amin;
+  float at_box_w, at_box_amax, at_box_amin;  // float32 box corners (jnp)
+  double ttr_max;
+  double cur_new[NCUR];
+  TableDev val, ttr;
+  StateDev s;
+  OutDev o;
+  const void* actions;
+};
+
+// ----------------------------------------------------------------------------------
+// LDS layout (dynamic, 16-byte aligned carve)
+// ----------------------------------------------------------------------------------
+struct Lds {
+  double* ps;        // [4][N] agent state (after integration; velocities pre-freeze)
+  double* lm;        // [4][NL]
+  double* lmsc;      // [2][NL] sin/cos of landmark headings
+  double* dist;      // [E][E]
+  double* raw;       // [2][N]
+  double* safe;      // [2][N]
+  double* dpair;     // [N][N]
+  float* vpair;      // [N][N]
+  uint8_t* inr;      // [N][N]
+  int32_t* dpre;     // [N] done before reward update
+  int32_t* dpost;    // [N] done after
+  int32_t* rpre;     // [N] reached_goal before
+  int32_t* rpost;    // [N] reached_goal after
+  double* wold;      // [2][N] dists_to_goal / times_required before this step's info
+  double* wnew;      // [2][N] after
+  double* scratch;   // [2][MAXN] for np.std
+  float* stage;      // [64][F]
+  uint32_t* mt;      // [MT_WORDS]
+  double* cur;       // [NCUR]
+};
+
+__host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
+
+__host__ __device__ inline size_t lds_bytes(int N, int NL, int E, int F) {
+  size_t b = 0;
+  b += align16(sizeof(double) * 4 * N);
+  b += align16(sizeof(double) * 4 * NL);
+  b += align16(sizeof(double) * 2 * NL);
+  b += align16(sizeof(double) * E * E);
+  b += align16(sizeof(double) * 2 * N) * 2;
+  b += align16(sizeof(double) * N * N);
+  b += align16(sizeof(float) * N * N);
+  b += align16(N * N);
+  b += align16(sizeof(int32_t) * N) * 4;
+  b += align16(sizeof(double) * 2 * N) * 2;
+  b += align16(sizeof(double) * 2 * MAXN);
+  b += align16(sizeof(float) * 64 * F);
+  b += align16(sizeof(uint32_t) * MT_WORDS);
+  b += align16(sizeof(double) * NCUR);
+  return b;
+}
+
+__device__ inline Lds carve(unsigned char* base, int N, int NL, int E, int F) {
+  Lds L;
+  size_t o = 0;
+  auto take = [&](size_t bytes) { unsigned char* p = base + o; o += align16(bytes); return p; };
+  L.ps = (double*)take(sizeof(double) * 4 * N);
+  L.lm = (double*)take(sizeof(double) * 4 * NL);
+  L.lmsc = (double*)take(sizeof(double) * 2 * NL);
+  L.dist = (double*)take(sizeof(double) * E * E);
+  L.raw = (double*)take(sizeof(double) * 2 * N);
+  L.safe = (double*)take(sizeof(double) * 2 * N);
+  L.dpair = (double*)take(sizeof(double) * N * N);
+  L.vpair = (float*)take(sizeof(float) * N * N);
+  L.inr = (uint8_t*)take(N * N);
+  L.dpre = (int32_t*)take(sizeof(int32_t) * N);
+  L.dpost = (int32_t*)take(sizeof(int32_t) * N);
+  L.rpre = (int32_t*)take(sizeof(int32_t) * N);
+  L.rpost = (int32_t*)take(sizeof(int32_t) * N);
+  L.wold = (double*)take(sizeof(double) * 2 * N);
+  L.wnew = (double*)take(sizeof(double) * 2 * N);
+  L.scratch = (double*)take(sizeof(double) * 2 * MAXN);
+  L.stage = (float*)take(sizeof(float) * 64 * F);
+  L.mt = (uint32_t*)take(sizeof(uint32_t) * MT_WORDS);
+  L.cur = (double*)take(sizeof(double) * NCUR);
+  return L;
+}
+
+enum { C_CR = 0, C_SLOPED, C_STAIR, C_RAT, C_RSC, C_GHE, C_GSE, C_MDT, C_SEP, C_ENG, C_FILT };
+
+// ----------------------------------------------------------------------------------
+// Wave-cooperative MT19937 (numpy legacy stream); all lanes run the same scalar sequence.
+// ----------------------------------------------------------------------------------
+struct WaveRng {
+  uint32_t* key;
+  int pos;
+  __device__ void gen() {
+    const int lane = threadIdx.x;
+    // phase A: i in [0, 227) reads old key[i], key[i+1], key[i+397]
+    for (int base = 0; base < MT_N - MT_M; base += WAVE) {
+      int i = base + lane;
+      uint32_t v = 0;
+      if (i < MT_N - MT_M) v = mt_twist1(key[i], key[i + 1], key[i + MT_M]);
+      __syncthreads();
+      if (i < MT_N - MT_M) key[i] = v;
+      __syncthreads();
+    }
+    // phases B, C: i in [227, 623) reads new key[i-227]
+    for (int base = MT_N - MT_M; base < MT_N - 1; base += WAVE) {
+      int i = base + lane;
+      uint32_t v = 0;
+      if (i < MT_N - 1) v = mt_twist1(key[i], key[i + 1], key[i + (MT_M - MT_N)]);
+      __syncthreads();
+      if (i < MT_N - 1) key[i] = v;
+      __syncthreads();
+    }
+    if (lane == 0) key[MT_N - 1] = mt_twist1(key[MT_N - 1], key[0], key[MT_M - 1]);
+    __syncthreads();
+    pos = 0;
+  }
+  __device__ uint32_t next32() {
+    if (pos >= MT_N) gen();
+    uint32_t y = key[pos];
+    pos++;
+    return mt_temper(y);
+  }
+  __device__ double next_double() {
+    uint32_t a = next32() >> 5;
+    uint32_t b = next32() >> 6;
+    return (a * 67108864.0 + b) / 9007199254740992.0;
+  }
+  __device__ double uniform(double lo, double hi) {
+    double range = hi - lo;
+    return lo + range * next_double();
+  }
+};
+
+// ----------------------------------------------------------------------------------
+// HJ grid interpolation (float32; semantics of oracle/hj_grid.py)
+// ----------------------------------------------------------------------------------
+template <int ND>
+__device__ inline bool grid_corners(const TableDev& T, const double* s, int* off, float* w) {
+  float wl[ND], wh[ND];
+  int il[ND], ih[ND];
+#pragma unroll
+  for (int d = 0; d < ND; ++d) {
+    float sd = (float)s[d];
+    float p = (sd - T.lo[d]) / T.sp[d];
+    if (!(p == p) || fabsf(p) > 1.0e9f) return false;
+    const int n = T.n[d];
+    float fl = floorf(p);
+    int f = (int)fl;
+    if (T.periodic[d]) {
+      wh[d] = p - (float)f;
+      int a = f % n;
+      if (a < 0) a += n;
+      int b = (f + 1) % n;
+      if (b < 0) b += n;
+      il[d] = a;
+      ih[d] = b;
+    } else {
+      if (p < 0.0f || p > (float)(n - 1)) return false;
+      if (f > n - 2) f = n - 2;
+      wh[d] = p - (float)f;
+      il[d] = f;
+      ih[d] = f + 1;
+    }
+    wl[d] = 1.0f - wh[d];
+  }
+#pragma unroll
+  for (int c = 0; c < (1 << ND); ++c) {
+    float ww = 0.0f;
+    int o = 0;
+#pragma unroll
+    for (int d = 0; d < ND; ++d) {
+      const int bit = (c >> (ND - 1 - d)) & 1;
+      const float wd = bit ? wh[d] : wl[d];
+      ww = (d == 0) ? wd : ww * wd;
+      o += (bit ? ih[d] : il[d]) * T.stride[d];
+    }
+    off[c] = o;
+    w[c] = ww;
+  }
+  return true;
+}
+
+template <int ND>
+__device__ inline bool interp_value(const TableDev& T, const double* s, float& out) {
+  int off[1 << ND];
+  float w[1 << ND];
+  if (!grid_corners<ND>(T, s, off, w)) return false;
+  float v[1 << ND];
+#pragma unroll
+  for (int c = 0; c < (1 << ND); ++c) v[c] = T.values[off[c]];
+  float acc = 0.0f;
+#pragma unroll
+  for (int c = 0; c < (1 << ND); ++c) acc = acc + w[c] * v[c];
+  out = acc;
+  return !(acc != acc);
+}
+
+template <int ND>
+__device__ inline void interp_grad(const TableDev& T, const double* s, float* g) {
+  int off[1 << ND];
+  float w[1 << ND];
+  for (int d = 0; d < ND; ++d) g[d] = 0.0f;
+  if (!grid_corners<ND>(T, s, off, w)) {
+    for (int d = 0; d < ND; ++d) g[d] = __builtin_nanf("");
+    return;
+  }
+#pragma unroll
+  for (int c = 0; c < (1 << ND); ++c) {
+    const float4 a = T.grads[(size_t)off[c] * T.gw];
+    float gv[8] = {a.x, a.y, a.z, a.w, 0.f, 0.f, 0.f, 0.f};
+    if (ND > 4) {
+      const float4 b = T.grads[(size_t)off[c] * T.gw + 1];
+      gv[4] = b.x; gv[5] = b.y; gv[6] = b.z; gv[7] = b.w;
+    }
+#pragma unroll
+    for (int d = 0; d < ND; ++d) g[d] = g[d] + w[c] * gv[d];
+  }
+}
+
+// ----------------------------------------------------------------------------------
+// per-agent helpers
+// ----------------------------------------------------------------------------------
+__device__ inline int goal_index(int reached, int j, int N, int NL) {
+  int order = reached * N + j;
+  if (order >= NL) order = (reached - 1) * N + j;
+  // the reference raises past the last landmark (use_masking=False only); clamp for safety
+  int g = (int)(int8_t)order;
+  return g < 0 ? 0 : (g >= NL ? NL - 1 : g);
+}
+
+// agent j velocity components for a given "post" choice.
+template <int DYN>
+__device__ inline void agent_vel(const Lds& S, int N, int j, bool post, double& vx, double& vy) {
+  const bool frozen = post && S.dpost[j];
+  if (DYN == 0) {
+    vx = frozen ? 0.0 : S.ps[2 * N + j];
+    vy = frozen ? 0.0 : S.ps[3 * N + j];
+  } else {
+    const double th = S.ps[2 * N + j];
+    const double sp = frozen ? 0.0 : S.ps[3 * N + j];
+    vx = sp * cos(th);
+    vy = sp * sin(th);
+  }
+}
+
+template <int DYN>
+__device__ inline double agent_speed(const Lds& S, int N, int j, bool post) {
+  const bool frozen = post && S.dpost[j];
+  if (DYN == 0) {
+    const double vx = frozen ? 0.0 : S.ps[2 * N + j];
+    const double vy = frozen ? 0.0 : S.ps[3 * N + j];
+    return sqrt(vx * vx + vy * vy);
+  }
+  return frozen ? 0.0 : S.ps[3 * N + j];
+}
+
+template <int DYN>
+__device__ inline double agent_theta(const Lds& S, int N, int j, bool post) {
+  if (DYN == 0) {
+    const bool frozen = post && S.dpost[j];
+    const double vx = frozen ? 0.0 : S.ps[2 * N + j];
+    const double vy = frozen ? 0.0 : S.ps[3 * N + j];
+    return atan2(vy, vx);
+  }
+  return S.ps[2 * N + j];
+}
+
+// evaluate_agent_goal_reached (navigation_graph_safe.py:606-656)
+template <int DYN>
+__device__ inline bool goal_reached(const KParams& P, const Lds& S, int i, bool post, int reached) {
+  const int N = P.N, NL = P.NL;
+  const int gi = goal_index(reached, i, N, NL);
+  const double gx = S.lm[gi], gy = S.lm[NL + gi], gh = S.lm[2 * NL + gi], gs = S.lm[3 * NL + gi];
+  const double px = S.ps[i], py = S.ps[N + i];
+  const double dist = plain_norm2(px - gx, py - gy);
+  const double th = agent_theta<DYN>(S, N, i, post);
+  const double he = dae(th, gh);
+  const double verr = fabs(agent_speed<DYN>(S, N, i, post) - gs);
+  const double mdt = S.cur[C_MDT], ghe = S.cur[C_GHE], gse = S.cur[C_GSE];
+  bool cond;
+  if (DYN == 0) {
+    const double d2 = blas_norm2(px - gx, py - gy);
+    if (d2 > mdt) {
+      cond = he < ghe;
+    } else if (gs > 0.2) {
+      cond = he < ghe;
+    } else {
+      const double sa = np_clip(1 - gs / 0.2, 0, 1);
+      const double tc = 0.5 * sa + ghe * (1 - sa);
+      const double da = np_clip(1 - d2 / mdt, 0, 1);
+      const double tca = tc * da + ghe * (1 - da);
+      cond = he < tca;
+    }
+  } else {
+    cond = he < ghe;
+  }
+  return dist < mdt && cond && verr < gse;
+}
+
+// double_integrator_velocity_error_from_magnetic_field_reference (utils.py:276-349)
+__device__ inline double magnetic_penalty(const KParams& P, double px, double py, double vx, double vy,
+                                          double gx, double gy, double gh, double gs, double radius) {
+  const double ch = cos(gh), sh = sin(gh);
+  double rpx, rpy, rvx, rvy;
+  blas_rot(ch, sh, px - gx, py - gy, rpx, rpy);
+  const double dist = blas_norm2(rpx, rpy);
+  const double polar = atan2(rpy, rpx);
+  blas_rot(ch, sh, vx - 0.0, vy - 0.0, rvx, rvy);
+  double href = 0.0;
+  if (!(fabs(rpx) < 1e-6)) {
+    const double x = 0.5 * rpx, y = rpy;
+    double m0 = 0.0, m1 = 0.0;
+    const double nr = -radius;
+    for (int k = 0; k < 50; ++k) {
+      const double Ly = nr * P.mag_c[k], Lz = nr * P.mag_s[k];
+      const double dLy = radius * P.mag_s[k], dLz = nr * P.mag_c[k];
+      const double r0 = x - 0.0, r1 = y - Ly, r2 = 0.0 - Lz;
+      const double r3 = pow(blas_norm3(r0, r1, r2), 3.0);
+      const double c0 = dLy * r2 - dLz * r1;
+      const double c1 = dLz * r0 - 0.0 * r2;
+      m0 += c0 / r3;
+      m1 += c1 / r3;
+    }
+    m0 = m0 / 0.5;
+    href = atan2(m1, m0);
+  }
+  double ref_speed = py_max(gs, 0.1);
+  const double dr = np_clip(dist / 1.5, 0, 1);
+  ref_speed = ref_speed * (1 - dr) + 1.0 * dr;
+  const double rfx = ref_speed * cos(href), rfy = ref_speed * sin(href);
+  const double err = blas_norm2(rvx - rfx, rvy - rfy);
+  const double cp = cos(polar);
+  if (cp < P.cos_pi6) return err;
+  const double ar = np_clip((cp - P.cos_pi6) / (1 - P.cos_pi6), 0, 1);
+  return err * (1 - ar) + dist * ar;
+}
+
+__device__ inline double seqdot4(const double* a, const double* b) {
+  double acc = 0.0;
+  for (int k = 0; k < 4; ++k) acc = acc + a[k] * b[k];
+  return acc;
+}
+
+// ----------------------------------------------------------------------------------
+// safety filter for one ego (lane), after pair scratch is filled
+// ----------------------------------------------------------------------------------
+template <int DYN>
+__device__ inline void rel_state(const Lds& S, int N, int e, int o, double* rel) {
+  const double ex = S.ps[e], ey = S.ps[N + e], e2 = S.ps[2 * N + e], e3 = S.ps[3 * N + e];
+  const double ox = S.ps[o], oy = S.ps[N + o], o2 = S.ps[2 * N + o], o3 = S.ps[3 * N + o];
+  if (DYN == 0) {
+    rel[0] = ex - ox; rel[1] = ey - oy; rel[2] = e2 - o2; rel[3] = e3 - o3;
+  } else {
+    const double d = sqrt((ox - ex) * (ox - ex) + (oy - ey) * (oy - ey));
+    const double rh = o2 - e2;
+    const double ang = atan2(oy - ey, ox - ex);
+    rel[0] = d * cos(ang - e2);
+    rel[1] = d * sin(ang - e2);
+    rel[2] = rh;
+    rel[3] = e3;
+    rel[4] = o3;
+  }
+}
+
+template <int DYN>
+__device__ inline void filter_ego(const KParams& P, Lds& S, int i, uint8_t& filtered, int& dec,
+                                  double& u0, double& u1) {
+  const int N = P.N;
+  u0 = S.raw[i];
+  u1 = S.raw[N + i];
+  filtered = 0;
+  dec = -1;
+  int jd = -1, jv = -1;
+  double dmin = 0.0;
+  float vmin = 0.0f;
+  for (int j = 0; j < N; ++j) {
+    if (j == i || S.dpre[j]) continue;
+    const double d = S.dpair[i * N + j];
+    const float v = S.vpair[i * N + j];
+    if (jd < 0 || d < dmin) { jd = j; dmin = d; }
+    if (jv < 0 || v < vmin) { jv = j; vmin = v; }
+  }
+  if (jd < 0) return;  // no other active agent
+  dec = jv;
+  if (dmin > P.coord_range) return;
+  if (!S.inr[i * N + jv]) return;
+  const int ND = (DYN == 0) ? 4 : 5;
+  double rel[5];
+  rel_state<DYN>(S, N, i, jv, rel);
+  double uref[4] = {S.raw[i], S.raw[N + i], S.raw[jv], S.raw[N + jv]};
+  float g[5];
+  if (DYN == 0) interp_grad<4>(P.val, rel, g); else interp_grad<5>(P.val, rel, g);
+  const float V = vmin;
+  double u[4];
+  bool alias = false;   // infeasible QP returns u_ref itself (safety_filter.py:304-305,373-375)
+  if (DYN == 0) {
+    if (V < 0.4f) {
+      const float dirv[4] = {g[2], g[3], -g[2], -g[3]};
+      for (int k = 0; k < 4; ++k) u[k] = (dirv[k] < 0.0f) ? -0.5 : 0.5;
+    } else {
+      const double a[4] = {(double)g[2], (double)g[3], -(double)g[2], -(double)g[3]};
+      const double c0 = (double)(float)rel[2], c1 = (double)(float)rel[3];
+      const double gg[4] = {(double)g[0], (double)g[1], (double)g[2], (double)g[3]};
+      const double cc[4] = {c0, c1, 0.0, 0.0};
+      const double b = seqdot4(gg, cc) + (double)(3.0f * V);
+      const double s = seqdot4(a, uref) + b;
+      if (s >= 0.0) {
+        for (int k = 0; k < 4; ++k) u[k] = uref[k];
+      } else {
+        double den = 0.0;
+        for (int k = 0; k < 4; ++k) den = den + a[k] * a[k] / 1.0;
+        if (den == 0.0) {
+          alias = true;
+          for (int k = 0; k < 4; ++k) u[k] = uref[k];
+        } else {
+          const double lam = s / den;
+          for (int k = 0; k < 4; ++k) u[k] = uref[k] - lam * (a[k] / 1.0);
+        }
+      }
+    }
+    const double axmax = (rel[2] < P.di_thr_xmax) ? P.di_axmax : 0.0;
+    const double axmin = (rel[2] > P.di_thr_xmin) ? P.di_axmin : 0.0;
+    u[0] = py_max(py_min(u[0], axmax), axmin);
+    const double aymax = (rel[3] < P.di_thr_ymax) ? P.di_aymax : 0.0;
+    const double aymin = (rel[3] > P.di_thr_ymin) ? P.di_aymin : 0.0;
+    u[1] = py_max(py_min(u[1], aymax), aymin);
+  } else {
+    const float s0 = (float)rel[0], s1 = (float)rel[1];
+    const float d0 = (g[0] * s1 + g[1] * (-s0)) + (-g[2]);
+    const float dirv[4] = {d0, g[2], g[3], g[4]};
+    bool f32u = false;
+    if (V < 0.4f) {
+      float lo[4] = {-P.at_box_w, -P.at_box_w, P.at_box_amin, P.at_box_amin};
+      float hi[4] = {P.at_box_w, P.at_box_w, P.at_box_amax, P.at_box_amax};
+      if (rel[4] >= P.at_vmax) hi[3] = 0.0f;
+      else if (rel[4] <= P.at_vmin) lo[3] = 0.0f;
+      else if (rel[3] >= P.at_vmax) hi[2] = 0.0f;
+      else if (rel[3] <= P.at_vmin) lo[2] = 0.0f;
+      for (int k = 0; k < 4; ++k) u[k] = (double)((dirv[k] < 0.0f) ? lo[k] : hi[k]);
+      f32u = true;
+    } else {
+      const float th32 = (float)rel[2];
+      const double ol0 = (double)(float)(-rel[3] + rel[4] * (double)cosf(th32));
+      const double ol1 = (double)(float)(rel[4] * (double)sinf(th32));
+      const double gg[5] = {(double)g[0], (double)g[1], (double)g[2], (double)g[3], (double)g[4]};
+      double a[4];
+      {
+        double acc = 0.0;
+        acc = acc + gg[0] * (double)s1;
+        acc = acc + gg[1] * (-(double)s0);
+        acc = acc + gg[2] * -1.0;
+        acc = acc + gg[3] * 0.0;
+        acc = acc + gg[4] * 0.0;
+        a[0] = acc;
+        for (int k = 1; k < 4; ++k) {
+          double t = 0.0;
+          for (int m = 0; m < 5; ++m) t = t + gg[m] * ((m == k + 1) ? 1.0 : 0.0);
+          a[k] = t;
+        }
+      }
+      double b = 0.0;
+      b = b + gg[0] * ol0;
+      b = b + gg[1] * ol1;
+      b = b + gg[2] * 0.0;
+      b = b + gg[3] * 0.0;
+      b = b + gg[4] * 0.0;
+      b = b + (double)(3.0f * V);
+      const double W0[4] = {100.0, 10.0, 10.0, 1.0};
+      const double W1[4] = {10.0, 1.0, 100.0, 10.0};
+      const double* W = (rel[0] < 0) ? W0 : W1;
+      const double s = seqdot4(a, uref) + b;
+      if (s >= 0.0) {
+        for (int k = 0; k < 4; ++k) u[k] = uref[k];
+        u[0] = py_max(py_min(u[0], P.at_wmax), -P.at_wmax);
+        u[2] = py_max(py_min(u[2], P.at_wmax), -P.at_wmax);
+      } else {
+        double den = 0.0;
+        for (int k = 0; k < 4; ++k) den = den + a[k] * a[k] / W[k];
+        if (den == 0.0) {
+          alias = true;
+          for (int k = 0; k < 4; ++k) u[k] = uref[k];
+        } else {
+          const double lam = s / den;
+          for (int k = 0; k < 4; ++k) u[k] = uref[k] - lam * (a[k] / W[k]);
+          u[0] = py_max(py_min(u[0], P.at_wmax), -P.at_wmax);
+          u[2] = py_max(py_min(u[2], P.at_wmax), -P.at_wmax);
+        }
+      }
+    }
+    double amax = (rel[3] < P.at_thr_amax) ? P.at_amax : 0.0;
+    double amin = (rel[3] > P.at_thr_amin) ? P.at_amin : 0.0;
+    u[1] = py_max(py_min(u[1], amax), amin);
+    if (f32u) u[1] = (double)(float)u[1];
+    amax = (rel[4] < P.at_thr_amax) ? P.at_amax : 0.0;
+    amin = (rel[4] > P.at_thr_amin) ? P.at_amin : 0.0;
+    u[3] = py_max(py_min(u[3], amax), amin);
+    if (f32u) u[3] = (double)(float)u[3];
+  }
+  if (alias) {
+    filtered = 0;
+  } else {
+    filtered = blas_norm4(u[0] - uref[0], u[1] - uref[1], u[2] - uref[2], u[3] - uref[3]) > 1e-4;
+  }
+  u0 = u[0];
+  u1 = u[1];
+  (void)ND;
+}
+
+// ----------------------------------------------------------------------------------
+// Outputs: per-ego node features + adjacency with the sequential snapshot rule.
+// ego i sees agent j "post" (after its reward update) iff j <= i.
+// ----------------------------------------------------------------------------------
+template <int DYN>
+__device__ inline void node_features(const KParams& P, const Lds& S, int e, int k, float* f) {
+  const int N = P.N, NL = P.NL;
+  const double pex = S.ps[e], pey = S.ps[N + e];
+  double vex, vey;
+  agent_vel<DYN>(S, N, e, true, vex, vey);
+  if (DYN == 0) {
+    if (k < N) {
+      const bool post = k <= e;
+      double vkx, vky;
+      agent_vel<DYN>(S, N, k, post, vkx, vky);
+      const int gi = goal_index(post ? S.rpost[k] : S.rpre[k], k, N, NL);
+      f[0] = (float)(S.ps[k] - pex);
+      f[1] = (float)(S.ps[N + k] - pey);
+      f[2] = (float)(vkx - vex);
+      f[3] = (float)(vky - vey);
+      f[4] = (float)(S.lm[gi] - pex);
+      f[5] = (float)(S.lm[NL + gi] - pey);
+      f[6] = (float)S.lmsc[gi];
+      f[7] = (float)S.lmsc[NL + gi];
+      f[8] = (float)S.lm[3 * NL + gi];
+      f[9] = 0.0f;
+    } else {
+      const int l = k - N;
+      const double rx = S.lm[l] - pex, ry = S.lm[NL + l] - pey;
+      f[0] = (float)rx;
+      f[1] = (float)ry;
+      f[2] = (float)(-vex);
+      f[3] = (float)(-vey);
+      f[4] = (float)rx;
+      f[5] = (float)ry;
+      f[6] = (float)S.lmsc[l];
+      f[7] = (float)S.lmsc[NL + l];
+      f[8] = (float)S.lm[3 * NL + l];
+      f[9] = 1.0f;
+    }
+  } else {
+    const double th = S.ps[2 * N + e];
+    const double c = cos(th), s = sin(th);
+    if (k < N) {
+      const bool post = k <= e;
+      double vkx, vky;
+      agent_vel<DYN>(S, N, k, post, vkx, vky);
+      const int gi = goal_index(post ? S.rpost[k] : S.rpre[k], k, N, NL);
+      double rx, ry, gx, gy;
+      blas_rot(c, s, S.ps[k] - pex, S.ps[N + k] - pey, rx, ry);
+      const double rh = S.ps[2 * N + k] - th;
+      const double rs = blas_norm2(vkx - vex, vky - vey);
+      blas_rot(c, s, S.lm[gi] - pex, S.lm[NL + gi] - pey, gx, gy);
+      const double rgh = S.lm[2 * NL + gi] - th;
+      f[0] = (float)rx;
+      f[1] = (float)ry;
+      f[2] = (float)rs;
+      f[3] = (float)sin(rh);
+      f[4] = (float)cos(rh);
+      f[5] = (float)gx;
+      f[6] = (float)gy;
+      f[7] = (float)sin(rgh);
+      f[8] = (float)cos(rgh);
+      f[9] = (float)S.lm[3 * NL + gi];
+      f[10] = 0.0f;
+    } else {
+      const int l = k - N;
+      double rx, ry;
+      blas_rot(c, s, S.lm[l] - pex, S.lm[NL + l] - pey, rx, ry);
+      const double rh = S.lm[2 * NL + l] - th;
+      const float sn = (float)sin(rh), cs = (float)cos(rh);
+      f[0] = (float)rx;
+      f[1] = (float)ry;
+      f[2] = (float)agent_speed<DYN>(S, N, e, true);
+      f[3] = sn;
+      f[4] = cs;
+      f[5] = (float)rx;
+      f[6] = (float)ry;
+      f[7] = sn;
+      f[8] = cs;
+      f[9] = (float)S.lm[3 * NL + l];
+      f[10] = 1.0f;
+    }
+  }
+}
+
+// entity r masked for ego e (snapshot)
+__device__ inline bool masked(const Lds& S, int N, int e, int r) {
+  if (r < N) return (r <= e) ? S.dpost[r] != 0 : S.dpre[r] != 0;
+  const int l = r - N;
+  const int a = l % N, order = l / N;
+  const int rg = (a <= e) ? S.rpost[a] : S.rpre[a];
+  return rg > order;
+}
+
+template <int DYN>
+__device__ void emit_graph(const KParams& P, Lds& S, int env) {
+  const int lane = threadIdx.x;
+  const int N = P.N, E = P.E, F = P.F;
+  // node features: pairs p = e * E + k, batches of 64 staged through LDS, then copied
+  const int npairs = N * E;
+  float* node_out = P.o.node + (size_t)env * npairs * F;
+  for (int b0 = 0; b0 < npairs; b0 += WAVE) {
+    const int p = b0 + lane;
+    if (p < npairs) {
+      float f[11];
+      node_features<DYN>(P, S, p / E, p % E, f);
+      for (int q = 0; q < F; ++q) S.stage[lane * F + q] = f[q];
+    }
+    __syncthreads();
+    const int cnt = min(WAVE, npairs - b0) * F;
+    for (int q = lane; q < cnt; q += WAVE) node_out[(size_t)b0 * F + q] = S.stage[q];
+    __syncthreads();
+  }
+  // adjacency: ego e, element u = r * E + c
+  const int EE = E * E;
+  float* adj_out = P.o.adj + (size_t)env * N * EE;
+  for (int e = 0; e < N; ++e) {
+    for (int u = lane; u < EE; u += WAVE) {
+      const int r = u / E, c = u - r * E;
+      float val = 0.0f;
+      if (!masked(S, N, e, r) && !masked(S, N, e, c)) {
+        const double d = S.dist[u];
+        if (d < P.coord_range && d > 0) val = (float)d;
+      }
+      adj_out[(size_t)e * EE + u] = val;
+    }
+  }
+}
+
+__device__ inline void compute_dist(const KParams& P, Lds& S) {
+  const int lane = threadIdx.x;
+  const int N = P.N, E = P.E, NL = P.NL;
+  for (int u = lane; u < E * E; u += WAVE) {
+    const int a = u / E, b = u - a * E;
+    double d = 0.0;
+    if (a != b) {
+      const int lo = a < b ? a : b, hi = a < b ? b : a;
+      const double xa = lo < N ? S.ps[lo] : S.lm[lo - N];
+      const double ya = lo < N ? S.ps[N + lo] : S.lm[NL + lo - N];
+      const double xb = hi < N ? S.ps[hi] : S.lm[hi - N];
+      const double yb = hi < N ? S.ps[N + hi] : S.lm[NL + hi - N];
+      const double dx = xa - xb, dy = ya - yb;
+      d = sqrt(dx * dx + dy * dy);
+    }
+    S.dist[u] = d;
+  }
+  __syncthreads();
+}
+
+template <int DYN>
+__device__ inline void write_obs(const KParams& P, const Lds& S, int env, int i) {
+  const int N = P.N, NL = P.NL;
+  const int gi = goal_index(S.rpre[i], i, N, NL);
+  const double gx = S.lm[gi], gy = S.lm[NL + gi], gh = S.lm[2 * NL + gi], gs = S.lm[3 * NL + gi];
+  float* o = P.o.obs + ((size_t)env * N + i) * P.OBS;
+  const double px = S.ps[i], py = S.ps[N + i];
+  if (DYN == 0) {
+    o[0] = (float)S.ps[2 * N + i];
+    o[1] = (float)S.ps[3 * N + i];
+    o[2] = (float)(gx - px);
+    o[3] = (float)(gy - py);
+    o[4] = (float)S.lmsc[gi];
+    o[5] = (float)S.lmsc[NL + gi];
+    o[6] = (float)gs;
+  } else {
+    const double th = S.ps[2 * N + i];
+    double rx, ry;
+    blas_rot(cos(th), sin(th), gx - px, gy - py, rx, ry);
+    const double rh = gh - th;
+    o[0] = (float)S.ps[3 * N + i];
+    o[1] = (float)rx;
+    o[2] = (float)ry;
+    o[3] = (float)sin(rh);
+    o[4] = (float)cos(rh);
+    o[5] = (float)gs;
+  }
+}
+
+__device__ inline void summary(const KParams& P, const double* st, int N, const int32_t* reached,
+                               double* scratch, double* out) {
+  // save_summary_of_episode (environment.py:895-911); st = stats [NSTAT][N]
+  const double* tl = st;
+  const double* td = st + N;
+  const double* dn = st + 2 * N;
+  const double* cf = st + 3 * N;
+  const double* md = st + 4 * N;
+  const double* mu = st + 5 * N;
+  double* a = scratch;
+  double* b = scratch + MAXN;
+  out[0] = P.dt * np_mean(tl, N);
+  out[1] = np_mean(td, N);
+  out[2] = np_mean(dn, N);
+  for (int i = 0; i < N; ++i) a[i] = (double)reached[i];
+  out[3] = np_mean(a, N);
+  for (int i = 0; i < N; ++i) b[i] = (tl[i] == 0) ? 1.0 : tl[i];
+  for (int i = 0; i < N; ++i) a[i] = cf[i] / b[i];
+  out[4] = np_mean(a, N);
+  out[5] = np_mean(md, N);
+  for (int i = 0; i < N; ++i) a[i] = mu[i] / b[i];
+  out[7] = np_mean(a, N);
+  if (out[5] == INFINITY) out[5] = P.coord_range;
+  double mn = md[0];
+  for (int i = 1; i < N; ++i) mn = (md[i] < mn) ? md[i] : mn;
+  out[6] = mn;
+  if (out[6] == INFINITY) out[6] = P.coord_range;
+}
+
+// Device reset of one env (MultiAgentGraphEnv.reset, environment.py:1046-1074).
+template <int DYN>
+__device__ void reset_env(const KParams& P, Lds& S, int env) {
+  const int lane = threadIdx.x;
+  const int N = P.N, NL = P.NL;
+  double* stats = P.s.stats + (size_t)env * NSTAT * N;
+  double* prev = P.s.prev + (size_t)env * 8;
+  // summary of the finishing episode (uses reached_goal before the reset)
+  if (lane == 0) {
+    double outv[8];
+    summary(P, stats, N, S.rpost, S.scratch, outv);
+    for (int k = 0; k < 8; ++k) prev[k] = outv[k];
+  }
+  // curriculum for this env
+  for (int k = lane; k < NCUR; k += WAVE) {
+    S.cur[k] = P.cur_new[k];
+    P.s.cur[(size_t)env * NCUR + k] = P.cur_new[k];
+  }
+  // RNG state -> LDS
+  const uint32_t* mtg = P.s.mt + (size_t)env * MT_WORDS;
+  for (int k = lane; k < MT_WORDS; k += WAVE) S.mt[k] = mtg[k];
+  __syncthreads();
+  WaveRng rng;
+  rng.key = S.mt;
+  rng.pos = (int)S.mt[MT_N];
+  ScenarioParams sp;
+  sp.dyn = DYN; sp.N = N; sp.L = P.L; sp.world_size = P.world_size; sp.coordination_range = P.coord_range;
+  sp.goal_speed_min = P.gs_min; sp.goal_speed_max = P.gs_max;
+  sp.ratio_airtaxi = S.cur[C_RAT]; sp.ratio_scenario = S.cur[C_RSC]; sp.two_pi = P.two_pi; sp.pi = P.pi;
+  // every lane runs the identical draw sequence and stores the identical values
+  random_scenario(rng, sp, S.ps, S.lm);
+  __syncthreads();
+  if (lane == 0) S.mt[MT_N] = (uint32_t)rng.pos;
+  __syncthreads();
+  uint32_t* mtw = P.s.mt + (size_t)env * MT_WORDS;
+  for (int k = lane; k < MT_WORDS; k += WAVE) mtw[k] = S.mt[k];
+  for (int k = lane; k < NL; k += WAVE) {
+    S.lmsc[k] = sin(S.lm[2 * NL + k]);
+    S.lmsc[NL + k] = cos(S.lm[2 * NL + k]);
+  }
+  for (int k = lane; k < N; k += WAVE) {
+    S.dpre[k] = 0; S.dpost[k] = 0; S.rpre[k] = 0; S.rpost[k] = 0;
+  }
+  __syncthreads();
+  compute_dist(P, S);
+  // per-agent reset of world metrics / stats / goal_min_time
+  if (lane < N) {
+    const int i = lane;
+    double* winfo = P.s.winfo + (size_t)env * NWINFO * N;
+    winfo[i] = -1.0; winfo[N + i] = -1.0; winfo[2 * N + i] = -1.0; winfo[3 * N + i] = 0.0;
+    for (int k = 0; k < NSTAT; ++k) stats[k * N + i] = (k == 4) ? INFINITY : 0.0;
+    P.s.pdist[(size_t)env * N + i] = 0.0;
+    const double gmt = plain_norm2(S.ps[i] - S.lm[i], S.ps[N + i] - S.lm[NL + i]) / P.max_speed;
+    P.s.gmt[(size_t)env * N + i] = gmt;
+    write_obs<DYN>(P, S, env, i);
+  }
+  if (lane == 0) {
+    P.s.step[env] = 0;
+    for (int k = 0; k < 8; ++k) P.o.ep_info[(size_t)env * 8 + k] = prev[k];
+  }
+  __syncthreads();
+  emit_graph<DYN>(P, S, env);
+}
+
+template <int DYN>
+__device__ void store_state(const KParams& P, const Lds& S, int env) {
+  const int lane = threadIdx.x;
+  const int N = P.N, NL = P.NL;
+  for (int k = lane; k < 4 * N; k += WAVE) {
+    const int c = k / N, j = k - c * N;
+    double v = S.ps[k];
+    if (S.dpost[j] && (DYN == 0 ? (c >= 2) : (c == 3))) v = 0.0;
+    P.s.st[(size_t)env * 4 * N + k] = v;
+    if (P.o.state) P.o.state[((size_t)env * N + j) * 4 + c] = v;
+  }
+  for (int k = lane; k < 4 * NL; k += WAVE) P.s.lm[(size_t)env * 4 * NL + k] = S.lm[k];
+  for (int k = lane; k < N; k += WAVE) {
+    P.s.done[(size_t)env * N + k] = (uint8_t)S.dpost[k];
+    P.s.reached[(size_t)env * N + k] = S.rpost[k];
+  }
+}
+
+template <int DYN>
+__global__ __launch_bounds__(64) void rollout_kernel(const KParams P) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int env = blockIdx.x;
+  const int lane = threadIdx.x;
+  const int N = P.N, NL = P.NL, E = P.E;
+  Lds S = carve(smem, N, NL, E, P.F);
+
+  // ---- load env state ------------------------------------------------------------
+  for (int k = lane; k < 4 * N; k += WAVE) S.ps[k] = P.s.st[(size_t)env * 4 * N + k];
+  for (int k = lane; k < 4 * NL; k += WAVE) S.lm[k] = P.s.lm[(size_t)env * 4 * NL + k];
+  for (int k = lane; k < N; k += WAVE) {
+    const int d = P.s.done[(size_t)env * N + k];
+    const int r = P.s.reached[(size_t)env * N + k];
+    S.dpre[k] = d; S.dpost[k] = d; S.rpre[k] = r; S.rpost[k] = r;
+  }
+  for (int k = lane; k < NCUR; k += WAVE) S.cur[k] = P.s.cur[(size_t)env * NCUR + k];
+  __syncthreads();
+
+  if (P.mode == 1) {
+    for (int k = lane; k < N; k += WAVE) S.rpost[k] = S.rpre[k];
+    __syncthreads();
+    reset_env<DYN>(P, S, env);
+    __syncthreads();
+    store_state<DYN>(P, S, env);
+    return;
+  }
+
+  for (int k = lane; k < NL; k += WAVE) {
+    S.lmsc[k] = sin(S.lm[2 * NL + k]);
+    S.lmsc[NL + k] = cos(S.lm[2 * NL + k]);
+  }
+
+  // ---- 1. update_graph() at step start (previous state, final masks) --------------
+  if (P.emit_edges) {
+    compute_dist(P, S);
+    uint8_t* eo = P.o.edges + (size_t)env * E * E;
+    for (int u = lane; u < E * E; u += WAVE) {
+      const int r = u / E, c = u - r * E;
+      double d = S.dist[u];
+      if (masked(S, N, N, r) || masked(S, N, N, c)) d = 0.0;
+      eo[u] = (d <= P.coord_range && d > 0) ? 1 : 0;
+    }
+  }
+
+  // ---- 2. decode actions ----------------------------------------------------------
+  if (lane < N) {
+    const size_t base = (size_t)env * N + lane;
+    int ai = 0;
+    if (P.action_kind == LSM_ACTIONS_INDEX_I32) {
+      ai = ((const int32_t*)P.actions)[base];
+    } else if (P.action_kind == LSM_ACTIONS_ONEHOT_F32) {
+      const float* a = (const float*)P.actions + base * 25;
+      float best = a[0];
+      for (int q = 1; q < 25; ++q) if (a[q] > best) { best = a[q]; ai = q; }
+    } else {
+      const double* a = (const double*)P.actions + base * 25;
+      double best = a[0];
+      for (int q = 1; q < 25; ++q) if (a[q] > best) { best = a[q]; ai = q; }
+    }
+    ai = ai < 0 ? 0 : (ai > 24 ? 24 : ai);
+    const int xi = ai / 5, yi = ai - xi * 5;
+    S.raw[lane] = P.act0[xi];
+    S.raw[N + lane] = P.act1[yi];
+  }
+  __syncthreads();
+
+  // ---- 3. safety filter ---------------------------------------------------------------
+  const bool filter_on = S.cur[C_FILT] != 0.0;
+  if (filter_on) {
+    const int npairs = N * N;
+    for (int p = lane; p < npairs; p += WAVE) {
+      const int i = p / N, j = p - i * N;
+      if (i == j || S.dpre[i] || S.dpre[j]) continue;
+      const double ex = S.ps[i], ey = S.ps[N + i], ox = S.ps[j], oy = S.ps[N + j];
+      S.dpair[p] = sqrt((ox - ex) * (ox - ex) + (oy - ey) * (oy - ey));
+      double rel[5];
+      rel_state<DYN>(S, N, i, j, rel);
+      float v = 0.0f;
+      bool ok;
+      if (DYN == 0) ok = interp_value<4>(P.val, rel, v); else ok = interp_value<5>(P.val, rel, v);
+      S.vpair[p] = ok ? v : INFINITY;
+      S.inr[p] = ok ? 1 : 0;
+    }
+    __syncthreads();
+  }
+  if (lane < N) {
+    const int i = lane;
+    double u0 = S.raw[i], u1 = S.raw[N + i];
+    if (filter_on) {
+      uint8_t fl = 0;
+      int dec = -1;
+      if (!S.dpre[i]) filter_ego<DYN>(P, S, i, fl, dec, u0, u1);
+      P.s.sfilt[(size_t)env * N + i] = fl;
+      P.s.decon[(size_t)env * N + i] = dec;
+    }
+    S.safe[i] = u0;
+    S.safe[N + i] = u1;
+    P.s.adiff[(size_t)env * N + i] = blas_norm2(S.raw[i] - u0, S.raw[N + i] - u1);
+  }
+  __syncthreads();
+
+  // ---- 4. integrate ----------------------------------------------------------------------
+  if (lane < N && !S.dpre[lane]) {
+    const int i = lane;
+    const double dt = P.dt;
+    const double a0 = S.safe[i], a1 = S.safe[N + i];
+    double x = S.ps[i], y = S.ps[N + i], s2 = S.ps[2 * N + i], s3 = S.ps[3 * N + i];
+    double spd;
+    if (DYN == 0) {
+      x = x + s2 * dt + 0.5 * a0 * dt * dt;
+      y = y + s3 * dt + 0.5 * a1 * dt * dt;
+      s2 = s2 + a0 * dt;
+      s3 = s3 + a1 * dt;
+      spd = sqrt(s2 * s2 + s3 * s3);
+      if (spd > P.max_speed) {
+        s2 = P.max_speed * s2 / spd;
+        s3 = P.max_speed * s3 / spd;
+      }
+      spd = sqrt(s2 * s2 + s3 * s3);
+    } else {
+      const double th0 = s2, v0 = s3, w = a0, ac = a1;
+      const double th1 = th0 + w * dt;
+      const double v1 = v0 + ac * dt;
+      if (w == 0.0) {
+        const double dd = v0 * dt + 0.5 * ac * dt * dt;
+        x = x + dd * cos(th0);
+        y = y + dd * sin(th0);
+      } else {
+        const double sn1 = sin(th1), cs1 = cos(th1), sn0 = sin(th0), cs0 = cos(th0);
+        x = x + (v1 * sn1 - v0 * sn0) / w + ac * (cs1 - cs0) / (w * w);
+        y = y + (-v1 * cs1 + v0 * cs0) / w + ac * (sn1 - sn0) / (w * w);
+      }
+      s2 = th1;
+      s3 = v1;
+      if (s3 > P.max_speed) s3 = P.max_speed;
+      if (s3 < P.min_speed) s3 = P.min_speed;
+      spd = s3;
+    }
+    S.ps[i] = x; S.ps[N + i] = y; S.ps[2 * N + i] = s2; S.ps[3 * N + i] = s3;
+    P.s.pdist[(size_t)env * N + i] += spd * dt;
+  }
+  __syncthreads();
+
+  // ---- 5. distances, min relative distance ---------------------------------------------
+  compute_dist(P, S);
+  if (lane < N) {
+    const int i = lane;
+    double m = INFINITY;
+    if (!S.dpre[i]) {
+      for (int j = 0; j < N; ++j) {
+        if (j == i || S.dpre[j]) continue;
+        const double d = blas_norm2(S.ps[i] - S.ps[j], S.ps[N + i] - S.ps[N + j]);
+        m = (d < m) ? d : m;
+      }
+    }
+    P.s.minrel[(size_t)env * N + i] = m;
+  }
+  const int cstep = P.s.step[env] + 1;
+
+  // ---- 6. obs, reward, goal/done update ---------------------------------------------------
+  double rew = 0.0;
+  if (lane < N) {
+    const int i = lane;
+    write_obs<DYN>(P, S, env, i);
+    const int gi = goal_index(S.rpre[i], i, N, NL);
+    const double gx = S.lm[gi], gy = S.lm[NL + gi], gh = S.lm[2 * NL + gi], gs = S.lm[3 * NL + gi];
+    const double px = S.ps[i], py = S.ps[N + i];
+    const double th = agent_theta<DYN>(S, N, i, false);
+    const double spd = agent_speed<DYN>(S, N, i, false);
+    const double he = dae(th, gh);
+    const double hpr = 1 - np_clip(he / S.cur[C_GHE], 0, 1);
+    const double se = fabs(spd - gs);
+    const double sen = np_clip(se / S.cur[C_GSE], 0, 1);
+    const double cra = P.use_filter_arg ? 1.0 : S.cur[C_RAT];
+    const bool reached = goal_reached<DYN>(P, S, i, false, S.rpre[i]);
+    const bool done0 = S.dpre[i] != 0;
+    double r = 0.0;
+    if (reached) {
+      const double spr = 1 - sen;
+      const double ddx = gx - px, ddy = gy - py;
+      double cte = ddx * sin(th) - ddy * cos(th);
+      cte = fabs(cte) / np_maximum(blas_norm2(ddx, ddy), 1e-6);
+      const double ctp = 1 - np_clip(cte, 0, 1);
+      const double perf = hpr * spr * ctp;
+      const double grew = (DYN == 0) ? 50 * perf : 50 * (perf * cra + (1 - cra));
+      if (!P.use_masking || !done0) r = r + grew;
+    }
+    if (!done0) {
+      if (DYN == 0) {
+        if (!P.use_filter_arg) {
+          double vx, vy;
+          agent_vel<DYN>(S, N, i, false, vx, vy);
+          double pen = 3 * magnetic_penalty(P, px, py, vx, vy, gx, gy, gh, gs, 2 * S.cur[C_MDT]);
+          pen = np_clip(1 - S.cur[C_SLOPED], 0, 1) * pen;
+          r = r - pen;
+        }
+        r = P.use_filter_arg ? r - 1.0 : r - 1.0 * S.cur[C_SLOPED];
+      } else {
+        double rpx, rpy;
+        blas_rot(cos(gh), sin(gh), px - gx, py - gy, rpx, rpy);
+        const double rs[4] = {rpx, rpy, th - gh, spd};
+        float ttr = 0.0f;
+        if (interp_value<4>(P.ttr, rs, ttr)) {
+          // reference: `rew -= 0.04 * ttr` with ttr a float32 (JAX) scalar: the product is
+          // float32; a python-int `rew` (no goal reward added) stays float32
+          const double ttrd = (double)(0.04f * ttr);
+          r = (reached && (!P.use_masking || !done0)) ? r - ttrd : (double)(float)(r - ttrd);
+        } else {
+          r = r - 0.04 * P.ttr_max;
+        }
+        r = r - sen * cra;
+      }
+    }
+    rew = np_clip(r, -40.0, 50.0);
+    int rp = S.rpre[i];
+    if (reached && (!P.use_masking || !done0)) rp += 1;
+    S.rpost[i] = rp;
+    S.dpost[i] = (rp >= P.L) ? 1 : S.dpre[i];
+    P.o.rew[(size_t)env * N + i] = (float)rew;
+  }
+  __syncthreads();
+
+  // ---- 7/8. info_callback numbers -----------------------------------------------------
+  if (lane < N) {
+    const int i = lane;
+    double* winfo = P.s.winfo + (size_t)env * NWINFO * N;
+    const double tr_old = winfo[i], dg_old = winfo[N + i];
+    S.wold[i] = dg_old; S.wold[N + i] = tr_old;
+    double tr = tr_old, dg = dg_old, dl = winfo[2 * N + i];
+    const int gi = goal_index(S.rpost[i], i, N, NL);
+    const double dist = plain_norm2(S.ps[i] - S.lm[gi], S.ps[N + i] - S.lm[NL + gi]);
+    const double pd = P.s.pdist[(size_t)env * N + i];
+    if (goal_reached<DYN>(P, S, i, true, S.rpost[i]) && tr == -1) {
+      tr = cstep * P.dt;
+      dg = pd;
+      dl = dist;
+    }
+    if (tr == -1) {
+      dg = pd;
+      dl = dist;
+    }
+    double nc = winfo[3 * N + i];
+    for (int a = 0; a < N; ++a) {
+      if (a == i) continue;
+      if (blas_norm2(S.ps[i] - S.ps[a], S.ps[N + i] - S.ps[N + a]) < 1.05 * (0.05 + 0.05)) nc += 1;
+    }
+    winfo[i] = tr; winfo[N + i] = dg; winfo[2 * N + i] = dl; winfo[3 * N + i] = nc;
+    S.wnew[i] = dg; S.wnew[N + i] = tr;
+  }
+  __syncthreads();
+  if (lane < N) {
+    const int i = lane;
+    double* sc = S.scratch;  // per-lane private copies below
+    double dsnap[MAXN], tsnap[MAXN], tmp[MAXN];
+    for (int j = 0; j < N; ++j) {
+      dsnap[j] = (j <= i) ? S.wnew[j] : S.wold[j];
+      tsnap[j] = (j <= i) ? S.wnew[N + j] : S.wold[N + j];
+    }
+    (void)sc;
+    const double dm = np_mean(dsnap, N), ds = np_std(dsnap, N, tmp);
+    const double tm = np_mean(tsnap, N), ts = np_std(tsnap, N, tmp);
+    double* inf = P.o.info + ((size_t)env * N + i) * LSM_INFO_FIELDS;
+    const double* winfo = P.s.winfo + (size_t)env * NWINFO * N;
+    const double mr = P.s.minrel[(size_t)env * N + i];
+    inf[LSM_INFO_INDIVIDUAL_REWARD] = rew;
+    inf[LSM_INFO_MIN_RELATIVE_DISTANCE] = mr;
+    inf[LSM_INFO_DIST_TO_GOAL] = winfo[2 * N + i];
+    inf[LSM_INFO_TIME_REQ_TO_GOAL] = winfo[i];
+    inf[LSM_INFO_NUM_AGENT_COLLISIONS] = winfo[3 * N + i];
+    inf[LSM_INFO_DISTANCE_MEAN] = dm;
+    inf[LSM_INFO_DISTANCE_VARIANCE] = ds;
+    inf[LSM_INFO_DISTS_TRAVELED] = winfo[N + i];
+    inf[LSM_INFO_TIME_MEAN] = tm;
+    inf[LSM_INFO_TIME_STDDEV] = ts;
+    inf[LSM_INFO_MIN_TIME_TO_GOAL] = P.s.gmt[(size_t)env * N + i];
+    inf[LSM_INFO_SAFETY_FILTERED] = (double)P.s.sfilt[(size_t)env * N + i];
+    inf[LSM_INFO_SAFETY_VIOLATED] = (mr < S.cur[C_SEP]) ? 1.0 : 0.0;
+    inf[LSM_INFO_DECONFLICTING_INDEX] = (double)P.s.decon[(size_t)env * N + i];
+    inf[LSM_INFO_ACTION_DIFF] = P.s.adiff[(size_t)env * N + i];
+    inf[LSM_INFO_REACHED_GOAL] = (double)S.rpost[i];
+  }
+
+  // ---- episode stats (environment.py:1004-1022), dones ---------------------------------
+  bool my_done = true;
+  if (lane < N) {
+    const int i = lane;
+    double* stats = P.s.stats + (size_t)env * NSTAT * N;
+    if (!S.dpost[i]) {  // departed is always True in the training scenario
+      stats[i] += 1;
+      double vx, vy;
+      agent_vel<DYN>(S, N, i, true, vx, vy);
+      stats[N + i] += blas_norm2(vx, vy) * P.dt;
+      int cnt = 0, neng = 0;
+      double mn = INFINITY;
+      for (int j = 0; j < N; ++j) {
+        if (masked(S, N, i, i) || masked(S, N, i, j)) continue;
+        const double d = S.dist[i * E + j];
+        if (!(d < P.coord_range && d > 0)) continue;
+        cnt++;
+        if (d < P.world_eng) neng++;
+        mn = (d < mn) ? d : mn;
+      }
+      if (cnt > 0) {
+        if (neng > 1) stats[5 * N + i] += 1;
+        if (mn < P.sep_target) stats[3 * N + i] += 1;
+        if (mn < stats[4 * N + i]) stats[4 * N + i] = mn;
+      }
+    }
+    if (S.dpost[i]) stats[2 * N + i] = 1;
+    my_done = S.dpost[i] || cstep >= P.episode_length;
+    P.o.dones[(size_t)env * N + i] = my_done ? 1 : 0;
+  }
+  const bool all_done = __all(my_done);
+  __syncthreads();
+
+  // ---- 9. graph outputs, then optional auto-reset -----------------------------------------
+  if (lane == 0) P.s.step[env] = cstep;
+  if (P.auto_reset && all_done) {
+    if (lane == 0) P.o.reset_flag[env] = 1;
+    reset_env<DYN>(P, S, env);
+    __syncthreads();
+    store_state<DYN>(P, S, env);
+  } else {
+    if (lane == 0) P.o.reset_flag[env] = 0;
+    emit_graph<DYN>(P, S, env);
+    __syncthreads();
+    store_state<DYN>(P, S, env);
+  }
+}
+
+// env k's MT19937: np.random.seed(seed + 1000 * (env_offset + k))
+__global__ void seed_kernel(uint32_t* mt, int n_envs, int64_t seed, int64_t env_offset) {
+  const int env = blockIdx.x * blockDim.x + threadIdx.x;
+  if (env >= n_envs) return;
+  const uint32_t s = (uint32_t)(seed + 1000 * (env_offset + env));
+  uint32_t* key = mt + (size_t)env * MT_WORDS;
+  mt_seed(s, key, 1);
+  key[MT_N] = MT_N;
+}
+
+}  // namespace lsm
+
+// ====================================================================================
+// C ABI
+// ====================================================================================
+using namespace lsm;
+
+struct lsm_env {
+  lsm_config cfg;
+  int N, L, NL, E, F, OBS;
+  StateDev s;
+  std::vector<void*> allocs;
+  void* out_ptr[LSM_NUM_OUT];
+  size_t out_bytes[LSM_NUM_OUT];
+  TableDev val, ttr;
+  double ttr_max;
+  std::string err;
+  bool tables_ok;
+  int device;
+};
+
+static int fail(lsm_env* e, const std::string& msg) {
+  if (e) e->err = msg;
+  return 1;
+}
+
+#define HIPCHK(env, expr)                                                              \
+  do {                                                                                 \
+    hipError_t _e = (expr);                                                            \
+    if (_e != hipSuccess) return fail(env, std::string(#expr) + ": " + hipGetErrorString(_e)); \
+  } while (0)
+
+template <class T>
+static int dalloc(lsm_env* e, T** p, size_t count) {
+  void* q = nullptr;
+  hipError_t r = hipMalloc(&q, count * sizeof(T) + 16);
+  if (r != hipSuccess) return fail(e, std::string("hipMalloc: ") + hipGetErrorString(r));
+  e->allocs.push_back(q);
+  *p = (T*)q;
+  return 0;
+}
+
+static void fill_params(const lsm_env* e, KParams& P) {
+  memset(&P, 0, sizeof(P));
+  const bool di = e->cfg.dynamics == LSM_DOUBLE_INTEGRATOR;
+  P.n_envs = e->cfg.num_envs;
+  P.N = e->N; P.L = e->L; P.NL = e->NL; P.E = e->E; P.F = e->F; P.OBS = e->OBS;
+  P.dyn = di ? 0 : 1;
+  P.episode_length = e->cfg.episode_length;
+  P.use_masking = e->cfg.use_masking;
+  P.use_filter_arg = e->cfg.use_safety_filter;
+  P.auto_reset = e->cfg.auto_reset;
+  P.emit_edges = e->cfg.emit_edges && e->out_ptr[LSM_OUT_EDGES] != nullptr;
+  P.world_size = e->cfg.world_size;
+  const double pi = 3.141592653589793;
+  P.pi = pi;
+  P.two_pi = 2 * pi;
+  if (di) {
+    P.dt = 0.1; P.coord_range = 4; P.world_eng = 1.0; P.sep_target = 0.5;
+    P.max_speed = 0.5; P.min_speed = 0.0; P.gs_min = 0.1; P.gs_max = 0.5;
+    const double opts[5] = {-0.5, -0.25, 0.0, 0.25, 0.5};   // np.linspace(-0.5, 0.5, 5)
+    for (int k = 0; k < 5; ++k) { P.act0[k] = opts[k]; P.act1[k] = opts[k]; }
+  } else {
+    P.dt = 1.0; P.coord_range = 3 * 1.60934; P.world_eng = 1.4; P.sep_target = 1500 * 0.0003048;
+    P.max_speed = 175 * 0.514444 * 0.001; P.min_speed = 60 * 0.514444 * 0.001;
+    P.gs_min = 60 * 0.514444 * 0.001; P.gs_max = 110 * 0.514444 * 0.001;
+    // np.linspace(-0.1, 0.1, 5), np.linspace(-0.001, 0.002, 5)
+    const double lo = -0.1, hi = 0.1, alo = -0.001, ahi = 0.002;
+    for (int k = 0; k < 5; ++k) {
+      P.act0[k] = (k == 4) ? hi : lo + k * ((hi - lo) / 4);
+      P.act1[k] = (k == 4) ? ahi : alo + k * ((ahi - alo) / 4);
+    }
+  }
+  P.cos_pi6 = cos(pi / 6);
+  for (int k = 0; k < 50; ++k) {
+    const double ph = k * ((2 * pi - 0) / 50);   // np.linspace(0, 2pi, 50, endpoint=False)
+    P.mag_c[k] = cos(ph);
+    P.mag_s[k] = sin(ph);
+  }
+  P.di_thr_xmax = 0.5 - 0.1 * 0.5; P.di_thr_xmin = -0.5 - 0.1 * -0.5;
+  P.di_thr_ymax = 0.5 - 0.1 * 0.5; P.di_thr_ymin = -0.5 - 0.1 * -0.5;
+  P.di_axmax = 0.5; P.di_axmin = -0.5; P.di_aymax = 0.5; P.di_aymin = -0.5;
+  P.at_vmax = 175 * 0.514444 * 0.001; P.at_vmin = 60 * 0.514444 * 0.001;
+  P.at_amax = 0.002; P.at_amin = -0.001; P.at_wmax = 0.1;
+  P.at_thr_amax = P.at_vmax - 1.0 * 0.002; P.at_thr_amin = P.at_vmin - 1.0 * -0.001;
+  P.at_box_w = (float)0.1; P.at_box_amax = (float)0.002; P.at_box_amin = (float)-0.001;
+  P.ttr_max = e->ttr_max;
+  P.val = e->val;
+  P.ttr = e->ttr;
+  P.s = e->s;
+  P.o.obs = (float*)e->out_ptr[LSM_OUT_OBS];
+  P.o.node = (float*)e->out_ptr[LSM_OUT_NODE_OBS];
+  P.o.adj = (float*)e->out_ptr[LSM_OUT_ADJ];
+  P.o.rew = (float*)e->out_ptr[LSM_OUT_REWARD];
+  P.o.dones = (uint8_t*)e->out_ptr[LSM_OUT_DONE];
+  P.o.reset_flag = (uint8_t*)e->out_ptr[LSM_OUT_RESET_FLAG];
+  P.o.ep_info = (double*)e->out_ptr[LSM_OUT_EP_INFO];
+  P.o.info = (double*)e->out_ptr[LSM_OUT_INFO];
+  P.o.edges = (uint8_t*)e->out_ptr[LSM_OUT_EDGES];
+  P.o.state = (double*)e->out_ptr[LSM_OUT_STATE];
+}
+
+extern "C" {
+
+size_t lsm_output_bytes(const lsm_env* e, int32_t slot) {
+  const size_t n = e->cfg.num_envs, N = e->N, E = e->E;
+  switch (slot) {
+    case LSM_OUT_OBS: return n * N * e->OBS * 4;
+    case LSM_OUT_NODE_OBS: return n * N * E * e->F * 4;
+    case LSM_OUT_ADJ: return n * N * E * E * 4;
+    case LSM_OUT_REWARD: return n * N * 4;
+    case LSM_OUT_DONE: return n * N;
+    case LSM_OUT_RESET_FLAG: return n;
+    case LSM_OUT_EP_INFO: return n * 8 * 8;
+    case LSM_OUT_INFO: return n * N * LSM_INFO_FIELDS * 8;
+    case LSM_OUT_EDGES: return n * E * E;
+    case LSM_OUT_STATE: return n * N * 4 * 8;
+    default: return 0;
+  }
+}
+
+int32_t lsm_num_entities(const lsm_env* e) { return e->E; }
+int32_t lsm_node_features(const lsm_env* e) { return e->F; }
+int32_t lsm_obs_dim(const lsm_env* e) { return e->OBS; }
+const char* lsm_last_error(const lsm_env* e) { return e ? e->err.c_str() : "null handle"; }
+
+int lsm_create(const lsm_config* cfg, lsm_env** out) {
+  *out = nullptr;
+  if (!cfg) return 1;
+  lsm_env* e = new lsm_env();
+  *out = e;
+  e->cfg = *cfg;
+  e->tables_ok = false;
+  e->ttr_max = 0.0;
+  memset(&e->val, 0, sizeof(e->val));
+  memset(&e->ttr, 0, sizeof(e->ttr));
+  for (int k = 0; k < LSM_NUM_OUT; ++k) { e->out_ptr[k] = nullptr; e->out_bytes[k] = 0; }
+  const int N = cfg->num_agents, L = cfg->num_landmarks;
+  if (cfg->dynamics != LSM_DOUBLE_INTEGRATOR && cfg->dynamics != LSM_AIRTAXI)
+    return fail(e, "dynamics must be LSM_DOUBLE_INTEGRATOR or LSM_AIRTAXI");
+  if (N < 2 || N > MAXN) return fail(e, "num_agents must be in [2, 32] for the one-wave kernel");
+  if (L < 2 || L > MAX_L) return fail(e, "num_landmarks must be in [2, 8] (reference asserts > 1)");
+  if (N * (1 + L) > MAXE) return fail(e, "N * (1 + L) must be <= 64 for the one-wave kernel");
+  if (N * L > 127) return fail(e, "landmark ids go through np.int8 (navigation_graph_safe.py:581)");
+  if (cfg->num_envs < 1) return fail(e, "num_envs must be >= 1");
+  if (cfg->episode_length < 1) return fail(e, "episode_length must be >= 1");
+  e->N = N; e->L = L; e->NL = N * L; e->E = N * (1 + L);
+  e->F = cfg->dynamics == LSM_DOUBLE_INTEGRATOR ? 10 : 11;
+  e->OBS = cfg->dynamics == LSM_DOUBLE_INTEGRATOR ? 7 : 6;
+  HIPCHK(e, hipGetDevice(&e->device));
+  const size_t n = cfg->num_envs;
+  int r = 0;
+  r |= dalloc(e, &e->s.st, n * 4 * N);
+  r |= dalloc(e, &e->s.pdist, n * N);
+  r |= dalloc(e, &e->s.done, n * N);
+  r |= dalloc(e, &e->s.reached, n * N);
+  r |= dalloc(e, &e->s.lm, n * 4 * e->NL);
+  r |= dalloc(e, &e->s.gmt, n * N);
+  r |= dalloc(e, &e->s.step, n);
+  r |= dalloc(e, &e->s.cur, n * NCUR);
+  r |= dalloc(e, &e->s.stats, n * NSTAT * N);
+  r |= dalloc(e, &e->s.prev, n * 8);
+  r |= dalloc(e, &e->s.winfo, n * NWINFO * N);
+  r |= dalloc(e, &e->s.sfilt, n * N);
+  r |= dalloc(e, &e->s.decon, n * N);
+  r |= dalloc(e, &e->s.minrel, n * N);
+  r |= dalloc(e, &e->s.adiff, n * N);
+  r |= dalloc(e, &e->s.mt, n * MT_WORDS);
+  if (r) return 1;
+  HIPCHK(e, hipMemset(e->s.st, 0, n * 4 * N * 8));
+  HIPCHK(e, hipMemset(e->s.pdist, 0, n * N * 8));
+  HIPCHK(e, hipMemset(e->s.done, 0, n * N));
+  HIPCHK(e, hipMemset(e->s.reached, 0, n * N * 4));
+  HIPCHK(e, hipMemset(e->s.lm, 0, n * 4 * e->NL * 8));
+  HIPCHK(e, hipMemset(e->s.step, 0, n * 4));
+  HIPCHK(e, hipMemset(e->s.cur, 0, n * NCUR * 8));
+  HIPCHK(e, hipMemset(e->s.sfilt, 0, n * N));
+  HIPCHK(e, hipMemset(e->s.adiff, 0, n * N * 8));
+  {
+    // reference initial values: prev summary (environment.py:873-881), stats (init_episode_agent_info)
+    std::vector<double> prev(n * 8, 0.0), stats(n * NSTAT * N, 0.0), winfo(n * NWINFO * N, -1.0),
+        minrel(n * N, INFINITY), gmt(n * N, INFINITY);
+    std::vector<int32_t> decon(n * N, -1);
+    for (size_t k = 0; k < n; ++k) {
+      prev[k * 8 + 0] = cfg->episode_length;
+      for (int i = 0; i < N; ++i) {
+        stats[k * NSTAT * N + 4 * N + i] = INFINITY;
+        winfo[k * NWINFO * N + 3 * N + i] = 0.0;
+      }
+    }
+    HIPCHK(e, hipMemcpy(e->s.prev, prev.data(), prev.size() * 8, hipMemcpyHostToDevice));
+    HIPCHK(e, hipMemcpy(e->s.stats, stats.data(), stats.size() * 8, hipMemcpyHostToDevice));
+    HIPCHK(e, hipMemcpy(e->s.winfo, winfo.data(), winfo.size() * 8, hipMemcpyHostToDevice));
+    HIPCHK(e, hipMemcpy(e->s.minrel, minrel.data(), minrel.size() * 8, hipMemcpyHostToDevice));
+    HIPCHK(e, hipMemcpy(e->s.gmt, gmt.data(), gmt.size() * 8, hipMemcpyHostToDevice));
+    HIPCHK(e, hipMemcpy(e->s.decon, decon.data(), decon.size() * 4, hipMemcpyHostToDevice));
+  }
+  hipLaunchKernelGGL(seed_kernel, dim3((n + 255) / 256), dim3(256), 0, 0, e->s.mt, (int)n, cfg->seed,
+                     cfg->env_offset);
+  HIPCHK(e, hipGetLastError());
+  HIPCHK(e, hipDeviceSynchronize());
+  if (!cfg->use_safety_filter && cfg->dynamics == LSM_DOUBLE_INTEGRATOR) e->tables_ok = true;
+  return 0;
+}
+
+void lsm_destroy(lsm_env* e) {
+  if (!e) return;
+  for (void* p : e->allocs) hipFree(p);
+  delete e;
+}
+
+static int upload_table(lsm_env* e, TableDev& T, int32_t ndim, const double* lo, const double* hi,
+                        const int32_t* shape, const int32_t* periodic, const float* values,
+                        const float* grads) {
+  if (ndim < 1 || ndim > 5) return fail(e, "table ndim must be in [1, 5]");
+  memset(&T, 0, sizeof(T));
+  T.ndim = ndim;
+  size_t nodes = 1;
+  for (int d = 0; d < ndim; ++d) {
+    if (shape[d] < 2) return fail(e, "table dims must have >= 2 nodes");
+    nodes *= (size_t)shape[d];
+  }
+  size_t stride = 1;
+  for (int d = ndim - 1; d >= 0; --d) {
+    T.n[d] = shape[d];
+    T.stride[d] = (int)stride;
+    stride *= shape[d];
+    T.periodic[d] = periodic[d] ? 1 : 0;
+    const double sp = T.periodic[d] ? (hi[d] - lo[d]) / shape[d] : (hi[d] - lo[d]) / (shape[d] - 1.0);
+    T.lo[d] = (float)lo[d];
+    T.sp[d] = (float)sp;
+  }
+  if (nodes > (size_t)INT32_MAX) return fail(e, "table too large for 32-bit corner offsets");
+  float* dv = nullptr;
+  if (dalloc(e, &dv, nodes)) return 1;
+  HIPCHK(e, hipMemcpy(dv, values, nodes * 4, hipMemcpyHostToDevice));
+  T.values = dv;
+  if (grads) {
+    T.gw = ndim <= 4 ? 1 : 2;
+    float4* dg = nullptr;
+    if (dalloc(e, &dg, nodes * T.gw)) return 1;
+    HIPCHK(e, hipMemcpy(dg, grads, nodes * T.gw * 16, hipMemcpyHostToDevice));
+    T.grads = dg;
+  }
+  return 0;
+}
+
+int lsm_set_value_table(lsm_env* e, int32_t ndim, const double* lo, const double* hi, const int32_t* shape,
+                        const int32_t* periodic, const float* values, const float* grads) {
+  const int want = e->cfg.dynamics == LSM_DOUBLE_INTEGRATOR ? 4 : 5;
+  if (ndim != want) return fail(e, "value table must be 4-D (double integrator) or 5-D (airtaxi)");
+  if (!grads) return fail(e, "value table needs its gradient table");
+  if (upload_table(e, e->val, ndim, lo, hi, shape, periodic, values, grads)) return 1;
+  e->tables_ok = (e->cfg.dynamics == LSM_DOUBLE_INTEGRATOR) || e->ttr.values != nullptr;
+  return 0;
+}
+
+int lsm_set_ttr_table(lsm_env* e, int32_t ndim, const double* lo, const double* hi, const int32_t* shape,
+                      const int32_t* periodic, const float* values, double ttr_max) {
+  if (ndim != 4) return fail(e, "TTR table must be 4-D");
+  if (upload_table(e, e->ttr, ndim, lo, hi, shape, periodic, values, nullptr)) return 1;
+  e->ttr_max = ttr_max;
+  e->tables_ok = !e->cfg.use_safety_filter || e->val.values != nullptr;
+  return 0;
+}
+
+int lsm_bind_output(lsm_env* e, int32_t slot, void* ptr, size_t bytes) {
+  if (slot < 0 || slot >= LSM_NUM_OUT) return fail(e, "bad output slot");
+  const size_t need = lsm_output_bytes(e, slot);
+  if (ptr && bytes < need) return fail(e, "output buffer too small for slot " + std::to_string(slot));
+  e->out_ptr[slot] = ptr;
+  e->out_bytes[slot] = bytes;
+  return 0;
+}
+
+static int check_ready(lsm_env* e, bool stepping) {
+  if (!e->tables_ok) return fail(e, "HJ value table (filter on) / TTR table (airtaxi) not set");
+  const int req[] = {LSM_OUT_OBS, LSM_OUT_NODE_OBS, LSM_OUT_ADJ, LSM_OUT_REWARD, LSM_OUT_DONE,
+                     LSM_OUT_RESET_FLAG, LSM_OUT_EP_INFO, LSM_OUT_INFO};
+  for (int s : req)
+    if (!e->out_ptr[s]) return fail(e, "output slot " + std::to_string(s) + " not bound");
+  (void)stepping;
+  return 0;
+}
+
+static int launch(lsm_env* e, KParams& P, hipStream_t st) {
+  const size_t lds = lds_bytes(e->N, e->NL, e->E, e->F);
+  if (lds > 65536) return fail(e, "LDS footprint too large");
+  if (P.dyn == 0)
+    hipLaunchKernelGGL(rollout_kernel<0>, dim3(e->cfg.num_envs), dim3(WAVE), lds, st, P);
+  else
+    hipLaunchKernelGGL(rollout_kernel<1>, dim3(e->cfg.num_envs), dim3(WAVE), lds, st, P);
+  HIPCHK(e, hipGetLastError());
+  return 0;
+}
+
+int lsm_reset(lsm_env* e, const lsm_curriculum* cur, void* stream) {
+  if (!e || !cur) return 1;
+  if (check_ready(e, false)) return 1;
+  KParams P;
+  fill_params(e, P);
+  memcpy(P.cur_new, cur, sizeof(double) * NCUR);
+  P.mode = 1;
+  P.emit_edges = 0;
+  return launch(e, P, (hipStream_t)stream);
+}
+
+int lsm_step(lsm_env* e, const void* actions, int32_t kind, const lsm_curriculum* cur, void* stream) {
+  if (!e || !actions || !cur) return fail(e, "null argument");
+  if (kind < 0 || kind > 2) return fail(e, "bad action kind");
+  if (check_ready(e, true)) return 1;
+  KParams P;
+  fill_params(e, P);
+  memcpy(P.cur_new, cur, sizeof(double) * NCUR);
+  P.mode = 0;
+  P.action_kind = kind;
+  P.actions = actions;
+  return launch(e, P, (hipStream_t)stream);
+}
+
+int lsm_host_mt_uniforms(uint32_t seed, int32_t count, double lo, double hi, double* out) {
+  HostMT m;
+  m.seed(seed);
+  for (int k = 0; k < count; ++k) out[k] = m.uniform(lo, hi);
+  return 0;
+}
+
+int lsm_host_scenario(const lsm_config* cfg, const lsm_curriculum* cur, uint32_t seed, double* agent_state,
+                      double* landmarks) {
+  const int N = cfg->num_agents, L = cfg->num_landmarks, NL = N * L;
+  if (N < 2 || N > MAXN || L < 2 || L > MAX_L) return 1;
+  HostMT m;
+  m.seed(seed);
+  ScenarioParams sp;
+  const bool di = cfg->dynamics == LSM_DOUBLE_INTEGRATOR;
+  sp.dyn = di ? 0 : 1; sp.N = N; sp.L = L; sp.world_size = cfg->world_size;
+  sp.coordination_range = di ? 4.0 : 3 * 1.60934;
+  sp.goal_speed_min = di ? 0.1 : 60 * 0.514444 * 0.001;
+  sp.goal_speed_max = di ? 0.5 : 110 * 0.514444 * 0.001;
+  sp.ratio_airtaxi = cur->ratio_airtaxi; sp.ratio_scenario = cur->ratio_scenario;
+  sp.pi = 3.141592653589793; sp.two_pi = 2 * sp.pi;
+  std::vector<double> st(4 * N), lm(4 * NL);
+  random_scenario(m, sp, st.data(), lm.data());
+  for (int i = 0; i < N; ++i)
+    for (int c = 0; c < 4; ++c) agent_state[i * 4 + c] = st[c * N + i];
+  for (int k = 0; k < NL; ++k)
+    for (int c = 0; c < 4; ++c) landmarks[k * 4 + c] = lm[c * NL + k];
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,129 @@
+// lsm_scenario.h -- Scenario.random_scenario (navigation_graph_safe.py:1199-1367) and
+// randomly_generate_separated_positions (custom_scenarios/utils.py:39-68), replayed
+// draw-for-draw on numpy's legacy MT19937 stream of env k (seed + 1000 k).
+//
+// Written once for both targets: the reset kernel instantiates it with the
+// wave-cooperative RNG (all 64 lanes execute the identical scalar sequence, the
+// MT19937 twist is split across lanes), the host test entry point with HostMT.
+// Output layout is the device's SoA: st[c * N + i] (c = x, y, v_x|theta, v_y|v),
+// lm[c * NL + k] (c = x, y, heading, speed), landmark k = order * N + agent.
+#pragma once
+#include "lsm_numeric.h"
+
+namespace lsm {
+
+constexpr int MAX_L = 8;
+
+struct ScenarioParams {
+  int dyn;          // 0 DI, 1 airtaxi
+  int N, L;
+  double world_size;
+  double coordination_range;
+  double goal_speed_min, goal_speed_max;
+  double ratio_airtaxi;     // curriculum_ratio_airtaxi in random_scenario
+  double ratio_scenario;    // curriculum_ratio (1 with the filter, else sloped)
+  double two_pi, pi;
+};
+
+template <class Rng>
+LSM_HD void separated_positions(Rng& rng, int n, double x0, double x1, double y0, double y1,
+                                double dmin, double dmax, double (*pos)[2]) {
+  for (int i = 0; i < n; ++i) {
+    double x, y;
+    if (i > 0) {
+      for (int j = 0; j < 1000; ++j) {
+        x = rng.uniform(x0, x1);
+        y = rng.uniform(y0, y1);
+        double d = 0.0;
+        for (int k = 0; k < i; ++k) {
+          double dx = pos[k][0] - x, dy = pos[k][1] - y;
+          double dk = sqrt(dx * dx + dy * dy);
+          if (k == 0 || dk < d) d = dk;
+        }
+        if (d > dmin && d < dmax) break;
+      }
+    } else {
+      x = rng.uniform(x0, x1);
+      y = rng.uniform(y0, y1);
+    }
+    pos[i][0] = x;
+    pos[i][1] = y;
+  }
+}
+
+template <class Rng>
+LSM_HD void random_scenario(Rng& rng, const ScenarioParams& p, double* st, double* lm) {
+  const int N = p.N, L = p.L, NL = N * L;
+  const double ws = p.world_size;
+  const double cra = p.ratio_airtaxi;
+  for (int i = 0; i < N; ++i) {
+    if (p.dyn == 0) {
+      double x = rng.uniform(-0.8 * ws, 0.8 * ws);
+      double y = rng.uniform(-0.8 * ws, 0.8 * ws);
+      st[0 * N + i] = x; st[1 * N + i] = y; st[2 * N + i] = 0.0; st[3 * N + i] = 0.0;
+    } else {
+      double xmin = -0.5 * ws;
+      double xmax = 0.25 * ws * cra + 0.0 * (1 - cra) * ws;
+      double y = rng.uniform(-0.5 * ws, 0.5 * ws);
+      double x = rng.uniform(xmin, xmax);
+      double spd = rng.uniform(p.goal_speed_min, p.goal_speed_max);
+      double th = rng.uniform(0.0, p.two_pi);
+      st[0 * N + i] = x; st[1 * N + i] = y; st[2 * N + i] = th; st[3 * N + i] = spd;
+    }
+  }
+  double prev[MAX_L][2];
+  double gp[MAX_L][2];
+  double heads[MAX_L];
+  double speeds[MAX_L];
+  bool have_prev = false;
+  for (int i = 0; i < N; ++i) {
+    if (p.dyn == 0) {
+      separated_positions(rng, L, -0.5 * ws, 0.5 * ws, -0.5 * ws, 0.5 * ws,
+                          0.25 * p.coordination_range, 0.75 * p.coordination_range, gp);
+      if (have_prev)
+        for (int k = 0; k < L; ++k)
+          if (rng.uniform(0.0, 1.0) < 0.5) { gp[k][0] = prev[k][0]; gp[k][1] = prev[k][1]; }
+    } else {
+      double yw = 0.1 * (1 - cra) + 0.5 * cra;
+      separated_positions(rng, L, 0.0, 0.75 * ws, -yw * ws, yw * ws,
+                          0.5 * p.coordination_range, p.coordination_range, gp);
+      if (have_prev)
+        for (int k = 0; k < L; ++k)
+          if (rng.uniform(0.0, 1.0) < 0.5) { gp[k][0] = prev[k][0]; gp[k][1] = prev[k][1]; }
+      if (gp[0][0] > gp[1][0]) {
+        double tx = gp[0][0], ty = gp[0][1];
+        gp[0][0] = gp[1][0]; gp[0][1] = gp[1][1];
+        gp[1][0] = tx; gp[1][1] = ty;
+      }
+    }
+    for (int k = 0; k < L - 1; ++k) heads[k] = atan2(gp[k + 1][1] - gp[k][1], gp[k + 1][0] - gp[k][0]);
+    const double last = heads[L - 2];
+    const double cr = p.ratio_scenario;
+    if (p.dyn != 0) {
+      for (int k = 0; k < L; ++k) speeds[k] = p.goal_speed_max * 1.0;
+    } else {
+      double rnd[MAX_L];
+      for (int k = 0; k < L; ++k) rnd[k] = rng.uniform(p.goal_speed_min, p.goal_speed_max);
+      double var = rng.uniform(0.0, 1.0);
+      bool use_rnd = var < py_min(cr, 1 - 0.2);
+      for (int k = 0; k < L; ++k) speeds[k] = use_rnd ? rnd[k] : p.goal_speed_max * 1.0;
+      if (!use_rnd) speeds[L - 1] = p.goal_speed_min;
+    }
+    for (int k = 0; k < L - 1; ++k) {
+      double pr = (p.dyn == 0) ? cr * 0.25 * p.pi : cra * 0.1 * p.pi;
+      heads[k] += rng.uniform(-pr, pr);
+    }
+    heads[L - 1] = last;
+    for (int k = 0; k < L; ++k) {
+      int idx = k * N + i;
+      lm[0 * NL + idx] = gp[k][0];
+      lm[1 * NL + idx] = gp[k][1];
+      lm[2 * NL + idx] = heads[k];
+      lm[3 * NL + idx] = speeds[k];
+    }
+    for (int k = 0; k < L; ++k) { prev[k][0] = gp[k][0]; prev[k][1] = gp[k][1]; }
+    have_prev = true;
+  }
+}
+
+}  // namespace lsm

@@ -1,0 +1,92 @@
+"""ctypes binding of the C ABI in ``include/lsm_rollout.h`` (``liblsm_rollout.so``).
+
+This is the Python stub a maintainer of the reference would add (see
+INTEGRATION.md): plain pointers and sizes only, no torch types cross the ABI.
+The library is built in-tree by ``lsm.build`` (``hipcc --offload-arch=gfx950``);
+if it is missing the import fails loudly -- there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "csrc", "liblsm_rollout.so")
+
+LSM_DOUBLE_INTEGRATOR, LSM_AIRTAXI = 0, 1
+LSM_ACTIONS_INDEX_I32, LSM_ACTIONS_ONEHOT_F32, LSM_ACTIONS_ONEHOT_F64 = 0, 1, 2
+(OUT_OBS, OUT_NODE_OBS, OUT_ADJ, OUT_REWARD, OUT_DONE, OUT_RESET_FLAG, OUT_EP_INFO, OUT_INFO,
+ OUT_EDGES, OUT_STATE) = range(10)
+NUM_OUT = 10
+INFO_FIELDS = ("individual_reward", "min_relative_distance", "Dist_to_goal", "Time_req_to_goal",
+               "Num_agent_collisions", "Distance_mean", "Distance_variance", "Dists_traveled",
+               "Time_mean", "Time_stddev", "Min_time_to_goal", "Safety filtered", "Safety violated",
+               "deconflicting_agent_index", "action_diff", "reached_goal")
+
+# Every symbol include/lsm_rollout.h declares (checked by tests/test_capi.py).
+EXPORTED = ("lsm_create", "lsm_destroy", "lsm_last_error", "lsm_set_value_table", "lsm_set_ttr_table",
+            "lsm_bind_output", "lsm_output_bytes", "lsm_reset", "lsm_step", "lsm_num_entities",
+            "lsm_node_features", "lsm_obs_dim", "lsm_host_mt_uniforms", "lsm_host_scenario")
+
+
+class LsmConfig(C.Structure):
+    _fields_ = [("dynamics", C.c_int32), ("num_envs", C.c_int32), ("num_agents", C.c_int32),
+                ("num_landmarks", C.c_int32), ("episode_length", C.c_int32),
+                ("use_safety_filter", C.c_int32), ("use_masking", C.c_int32),
+                ("auto_reset", C.c_int32), ("emit_edges", C.c_int32), ("reserved0", C.c_int32),
+                ("world_size", C.c_double), ("seed", C.c_int64), ("env_offset", C.c_int64)]
+
+
+class LsmCurriculum(C.Structure):
+    _fields_ = [(n, C.c_double) for n in (
+        "curriculum_ratio", "sloped", "stair", "ratio_airtaxi", "ratio_scenario",
+        "goal_heading_error_thresh", "goal_speed_error_thresh", "min_dist_thresh",
+        "separation_distance", "engagement_distance", "world_use_safety_filter", "reserved")]
+
+
+class LsmError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def load_library(path: str = LIB_PATH):
+    """Load liblsm_rollout.so (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise LsmError("liblsm_rollout.so not built (%s); run __graft_entry__.build() or "
+                       "python -m lsm.build -- there is no CPU fallback" % path)
+    lib = C.CDLL(path)
+    P, I32, I64, U32, D, SZ = C.c_void_p, C.c_int32, C.c_int64, C.c_uint32, C.c_double, C.c_size_t
+    sig = {
+        "lsm_create": (I32, [C.POINTER(LsmConfig), C.POINTER(P)]),
+        "lsm_destroy": (None, [P]),
+        "lsm_last_error": (C.c_char_p, [P]),
+        "lsm_set_value_table": (I32, [P, I32, P, P, P, P, P, P]),
+        "lsm_set_ttr_table": (I32, [P, I32, P, P, P, P, P, D]),
+        "lsm_bind_output": (I32, [P, I32, P, SZ]),
+        "lsm_output_bytes": (SZ, [P, I32]),
+        "lsm_reset": (I32, [P, C.POINTER(LsmCurriculum), P]),
+        "lsm_step": (I32, [P, P, I32, C.POINTER(LsmCurriculum), P]),
+        "lsm_num_entities": (I32, [P]),
+        "lsm_node_features": (I32, [P]),
+        "lsm_obs_dim": (I32, [P]),
+        "lsm_host_mt_uniforms": (I32, [U32, I32, D, D, P]),
+        "lsm_host_scenario": (I32, [C.POINTER(LsmConfig), C.POINTER(LsmCurriculum), U32, P, P]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(rc: int, handle=None):
+    if rc != 0:
+        lib = load_library()
+        msg = lib.lsm_last_error(handle).decode() if handle else "lsm call failed"
+        raise LsmError(msg)

@@ -1,0 +1,261 @@
+"""``GpuGraphVecEnv`` -- drop-in for GraphSubprocVecEnv / GraphDummyVecEnv on one MI355X.
+
+Mirrors the reference's vec-env surface for the navigation_graph_safe path
+(``onpolicy/envs/env_wrappers.py:29-140,851-1029``):
+
+* ``reset(num_current_episode=0)`` -> ``(obs, agent_id, node_obs, adj, ep_info)``
+* ``step(actions, num_current_episode=None)`` -> the 7-tuple of
+  ``GraphSubprocVecEnv`` (auto-reset when every agent of an env is done, ep_info
+  appended as the (N+1)-th info entry) or, with ``auto_reset=False``, the 8-tuple
+  of ``GraphDummyVecEnv`` (``reset_count = 0``, no auto-reset)
+* ``step_async`` / ``step_wait`` / ``close`` and the space attributes the runner
+  sizes its buffers from.
+
+All computation happens in ``liblsm_rollout.so`` (C ABI, HIP kernels). This
+class only allocates the device output buffers (torch tensors), computes the
+per-call curriculum block with the reference's float64 expressions, and converts
+outputs: ``return_numpy=True`` gives host numpy arrays like the reference
+(float32 instead of float64 for obs/node_obs/adj/rewards -- the runner's buffer
+stores float32); ``return_numpy=False`` keeps everything as device tensors.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional
+
+import numpy as np
+
+from . import capi
+from .config import EnvArgs
+from .curriculum import curriculum_block, to_struct
+from .hj_tables import HjTable, default_tables
+from .spaces import Box, Discrete
+
+EPKEYS = ("travel_time_mean", "travel_distance_mean", "done_percentage", "num_reached_goal_mean",
+          "conflict_percentage", "min_distance_mean", "min_distance_min", "multiple_engagement_percentage")
+
+
+def _torch():
+    import torch
+    return torch
+
+
+class EnvInfos(list):
+    """Per-env info list built lazily from the device info tensor (host copy)."""
+
+
+class GpuGraphVecEnv:
+    def __init__(self, all_args, num_envs: Optional[int] = None, device=None,
+                 value_table: Optional[HjTable] = None, ttr_table: Optional[HjTable] = None,
+                 auto_reset: bool = True, env_offset: int = 0, emit_edges: bool = False,
+                 return_numpy: bool = True, build_infos: bool = True, small_tables: bool = False):
+        torch = _torch()
+        self.args = EnvArgs.from_namespace(all_args) if not isinstance(all_args, EnvArgs) else all_args
+        self.args.validate()
+        a = self.args
+        if a.num_landmarks < 2:
+            raise ValueError("num_landmarks must be >= 2 (reference asserts, utils.py:31)")
+        self.num_envs = int(num_envs if num_envs is not None else a.n_rollout_threads)
+        self.device = torch.device(device if device is not None else "cuda:%d" % torch.cuda.current_device())
+        if self.device.type != "cuda":
+            raise capi.LsmError("GpuGraphVecEnv needs a HIP device; there is no CPU fallback")
+        torch.cuda.set_device(self.device)
+        self.lib = capi.load_library()
+        self.auto_reset = bool(auto_reset)
+        self.return_numpy = bool(return_numpy)
+        self.build_infos = bool(build_infos)
+        di = a.dynamics_type == "double_integrator"
+        self.N = int(a.num_agents)
+        cfg = capi.LsmConfig(dynamics=capi.LSM_DOUBLE_INTEGRATOR if di else capi.LSM_AIRTAXI,
+                             num_envs=self.num_envs, num_agents=self.N, num_landmarks=int(a.num_landmarks),
+                             episode_length=int(a.episode_length), use_safety_filter=int(bool(a.use_safety_filter)),
+                             use_masking=int(bool(a.use_masking)), auto_reset=int(self.auto_reset),
+                             emit_edges=int(bool(emit_edges)), reserved0=0, world_size=float(a.world_size),
+                             seed=int(a.seed), env_offset=int(env_offset))
+        if int(a.seed) + 1000 * (int(env_offset) + self.num_envs - 1) >= 2 ** 32:
+            raise ValueError("numpy seeds must be < 2**32 (seed + 1000 * env index)")
+        h = C.c_void_p()
+        rc = self.lib.lsm_create(C.byref(cfg), C.byref(h))
+        self.h = h
+        capi.check(rc, h)
+        # HJ / TTR tables (synthetic stand-ins for the absent pickles unless given)
+        if a.use_safety_filter or not di:
+            vt, tt = default_tables(a.dynamics_type, small=small_tables)
+            value_table = value_table if value_table is not None else vt
+            ttr_table = ttr_table if ttr_table is not None else tt
+        self.value_table = value_table if a.use_safety_filter else None
+        self.ttr_table = ttr_table if not di else None
+        if self.value_table is not None:
+            self._upload_value_table()
+        if self.ttr_table is not None:
+            t = self.ttr_table
+            self._set_table(self.lib.lsm_set_ttr_table, t, t.values_hj, None, extra=float(t.ttr_max))
+        # outputs
+        self.E = int(self.lib.lsm_num_entities(h))
+        self.F = int(self.lib.lsm_node_features(h))
+        self.OBS = int(self.lib.lsm_obs_dim(h))
+        n, N, E, F = self.num_envs, self.N, self.E, self.F
+        dev = self.device
+        self.t_obs = torch.zeros((n, N, self.OBS), dtype=torch.float32, device=dev)
+        self.t_node = torch.zeros((n, N, E, F), dtype=torch.float32, device=dev)
+        self.t_adj = torch.zeros((n, N, E, E), dtype=torch.float32, device=dev)
+        self.t_rew = torch.zeros((n, N), dtype=torch.float32, device=dev)
+        self.t_done = torch.zeros((n, N), dtype=torch.uint8, device=dev)
+        self.t_reset = torch.zeros((n,), dtype=torch.uint8, device=dev)
+        self.t_epinfo = torch.zeros((n, 8), dtype=torch.float64, device=dev)
+        self.t_info = torch.zeros((n, N, len(capi.INFO_FIELDS)), dtype=torch.float64, device=dev)
+        self.t_state = torch.zeros((n, N, 4), dtype=torch.float64, device=dev)
+        self.t_edges = torch.zeros((n, E, E), dtype=torch.uint8, device=dev) if emit_edges else None
+        for slot, t in ((capi.OUT_OBS, self.t_obs), (capi.OUT_NODE_OBS, self.t_node),
+                        (capi.OUT_ADJ, self.t_adj), (capi.OUT_REWARD, self.t_rew),
+                        (capi.OUT_DONE, self.t_done), (capi.OUT_RESET_FLAG, self.t_reset),
+                        (capi.OUT_EP_INFO, self.t_epinfo), (capi.OUT_INFO, self.t_info),
+                        (capi.OUT_STATE, self.t_state), (capi.OUT_EDGES, self.t_edges)):
+            if t is None:
+                continue
+            capi.check(self.lib.lsm_bind_output(h, slot, C.c_void_p(t.data_ptr()),
+                                                t.numel() * t.element_size()), h)
+        self.agent_id = torch.arange(N, device=dev, dtype=torch.int64).view(1, N, 1).expand(n, N, 1).contiguous()
+        # spaces (environment.py:143-202, 928-960)
+        self.action_space = [Discrete(25) for _ in range(N)]
+        self.observation_space = [Box(-np.inf, np.inf, (self.OBS,)) for _ in range(N)]
+        self.share_observation_space = [Box(-np.inf, np.inf, (self.OBS * N,)) for _ in range(N)]
+        self.node_observation_space = [Box(-np.inf, np.inf, (E, F)) for _ in range(N)]
+        self.adj_observation_space = [Box(-np.inf, np.inf, (E, E)) for _ in range(N)]
+        self.edge_observation_space = [Box(-np.inf, np.inf, (1,)) for _ in range(N)]
+        self.agent_id_observation_space = [Box(-np.inf, np.inf, (1,)) for _ in range(N)]
+        self.share_agent_id_observation_space = [Box(-np.inf, np.inf, (N,)) for _ in range(N)]
+        self._pending = None
+        self._last_ep = 0
+        self._sep_tracked = None
+        self.closed = False
+
+    # -- tables ------------------------------------------------------------------------
+    def _set_table(self, fn, t: HjTable, values, grads, extra=None):
+        nd = t.ndim
+        lo = (C.c_double * nd)(*[float(x) for x in t.lo])
+        hi = (C.c_double * nd)(*[float(x) for x in t.hi])
+        shape = (C.c_int32 * nd)(*[int(x) for x in t.shape])
+        per = (C.c_int32 * nd)(*[1 if d in t.periodic else 0 for d in range(nd)])
+        v = np.ascontiguousarray(values, dtype=np.float32)
+        args = [self.h, nd, lo, hi, shape, per, v.ctypes.data_as(C.c_void_p)]
+        if grads is not None:
+            g = np.ascontiguousarray(grads, dtype=np.float32)
+            args.append(g.ctypes.data_as(C.c_void_p))
+        if extra is not None:
+            args.append(extra)
+        capi.check(fn(*args), self.h)
+
+    def _upload_value_table(self):
+        t = self.value_table
+        self._set_table(self.lib.lsm_set_value_table, t, t.values_hj, t.device_grads())
+
+    def _track_separation(self, block):
+        """HjDataHandle.update_separation_distance: values_hj -= shift (float32, in place)."""
+        if self.value_table is None:
+            return
+        sep = block["separation_distance"]
+        if self.value_table.shift_separation(sep) != 0:
+            self._upload_value_table()
+
+    # -- vec-env API -------------------------------------------------------------------------
+    def _stream(self):
+        return C.c_void_p(_torch().cuda.current_stream(self.device).cuda_stream)
+
+    def reset(self, num_current_episode: int = 0):
+        block = curriculum_block(self.args, num_current_episode)
+        self._track_separation(block)
+        self._last_ep = num_current_episode
+        cur = to_struct(block)
+        capi.check(self.lib.lsm_reset(self.h, C.byref(cur), self._stream()), self.h)
+        ep = self._ep_info_all()
+        if self.return_numpy:
+            return (self.t_obs.cpu().numpy(), self.agent_id.cpu().numpy(), self.t_node.cpu().numpy(),
+                    self.t_adj.cpu().numpy(), ep)
+        return self.t_obs, self.agent_id, self.t_node, self.t_adj, ep
+
+    def _ep_info_all(self):
+        e = self.t_epinfo.cpu().numpy()
+        return tuple({k: float(e[i, j]) for j, k in enumerate(EPKEYS)} for i in range(self.num_envs))
+
+    def _actions_device(self, actions):
+        torch = _torch()
+        if isinstance(actions, torch.Tensor):
+            t = actions.to(self.device)
+        else:
+            t = torch.as_tensor(np.asarray(actions), device=self.device)
+        if t.dim() == 2:
+            return t.to(torch.int32).contiguous(), capi.LSM_ACTIONS_INDEX_I32
+        if t.dim() == 3 and t.shape[-1] == 25:
+            if t.dtype == torch.float64:
+                return t.contiguous(), capi.LSM_ACTIONS_ONEHOT_F64
+            return t.to(torch.float32).contiguous(), capi.LSM_ACTIONS_ONEHOT_F32
+        raise ValueError("actions must be (n_envs, N) indices or (n_envs, N, 25) one-hot")
+
+    def step_async(self, actions, num_current_episode: Optional[int] = None):
+        ep = self._last_ep if num_current_episode is None else num_current_episode
+        block = curriculum_block(self.args, ep)
+        act, kind = self._actions_device(actions)
+        cur = to_struct(block)
+        capi.check(self.lib.lsm_step(self.h, C.c_void_p(act.data_ptr()), kind, C.byref(cur), self._stream()),
+                   self.h)
+        self._pending = (act, block)
+
+    def step_wait(self):
+        self._pending = None
+        if not self.return_numpy:
+            out = (self.t_obs, self.agent_id, self.t_node, self.t_adj, self.t_rew, self.t_done.bool(),
+                   (self.t_info, self.t_reset, self.t_epinfo))
+            return out + (0,) if not self.auto_reset else out
+        obs = self.t_obs.cpu().numpy()
+        node = self.t_node.cpu().numpy()
+        adj = self.t_adj.cpu().numpy()
+        rew = self.t_rew.cpu().numpy()
+        dones = self.t_done.cpu().numpy().astype(bool)
+        infos = self._infos() if self.build_infos else None
+        aid = self.agent_id.cpu().numpy()
+        if self.auto_reset:
+            return obs, aid, node, adj, rew, dones, infos
+        return obs, aid, node, adj, rew, dones, infos, 0
+
+    def step(self, actions, num_current_episode: Optional[int] = None):
+        self.step_async(actions, num_current_episode)
+        return self.step_wait()
+
+    def _infos(self):
+        info = self.t_info.cpu().numpy()
+        reset = self.t_reset.cpu().numpy()
+        ep = self.t_epinfo.cpu().numpy() if reset.any() else None
+        fields = capi.INFO_FIELDS
+        out = []
+        for e in range(self.num_envs):
+            lst = EnvInfos()
+            for i in range(self.N):
+                d = {k: float(info[e, i, j]) for j, k in enumerate(fields)}
+                d["Safety filtered"] = bool(d["Safety filtered"])
+                d["Safety violated"] = bool(d["Safety violated"])
+                d["id"] = i
+                d["Departed"] = True
+                d["Num_obst_collisions"] = 0.0
+                lst.append(d)
+            if self.auto_reset and reset[e]:
+                lst.append({k: float(ep[e, j]) for j, k in enumerate(EPKEYS)})
+            out.append(lst)
+        return tuple(out)
+
+    def state(self):
+        """Agent states [n, N, 4] (float64) after the last call (positions/velocities)."""
+        return self.t_state
+
+    def close(self):
+        if not self.closed and getattr(self, "h", None):
+            _torch().cuda.synchronize(self.device)
+            self.lib.lsm_destroy(self.h)
+            self.h = None
+        self.closed = True
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,185 @@
+"""GPU parity tests: the HIP path (through the C ABI) vs the reference's golden vectors and
+the CPU oracle. Tolerances (BASELINE.json north_star): graph edges / adjacency nonzero
+pattern / done masks bit-exact; fp32 outputs within 1e-5; float64 states within 1e-9
+(the kernel integrates in closed form, the reference with RK45: they differ by ~1e-16)."""
+import numpy as np
+import pytest
+
+from golden_replay import EPKEYS, INFOKEYS, adj_bits, fixture_names, load, table_dict, tables_for
+
+pytestmark = pytest.mark.gpu
+
+STATE_ATOL = 1e-9
+F32_ATOL = 1e-5
+
+
+def _gpu_env(meta, n_envs=1, seed=None, **kw):
+    from lsm.config import EnvArgs
+    from lsm.vec_env import GpuGraphVecEnv
+    args = EnvArgs.from_namespace(type("A", (), meta)())
+    args.seed = meta["env_seed"] if seed is None else seed
+    vt, tt = tables_for(meta)
+    return GpuGraphVecEnv(args, num_envs=n_envs, device="cuda:0", value_table=vt, ttr_table=tt, **kw)
+
+
+def _info_col(name):
+    from lsm import capi
+    return capi.INFO_FIELDS.index(name)
+
+
+GPU_FIXTURES = [n for n in fixture_names() if "inject" not in n]
+
+
+@pytest.mark.parametrize("name", GPU_FIXTURES)
+def test_gpu_matches_reference_golden(name):
+    z, meta = load(name)
+    env = _gpu_env(meta, emit_edges=True)
+    obs, aid, node, adj, ep = env.reset(meta["ep"])
+    np.testing.assert_allclose(obs[0], z["reset0_obs"], rtol=0, atol=F32_ATOL)
+    np.testing.assert_allclose(node[0], z["reset0_node"], rtol=0, atol=F32_ATOL)
+    np.testing.assert_allclose(adj[0], z["reset0_adj"], rtol=0, atol=F32_ATOL)
+    np.testing.assert_array_equal(adj[0] != 0, z["reset0_adj"] != 0)
+    np.testing.assert_allclose(env.state().cpu().numpy()[0], z["reset0_state"], rtol=0, atol=STATE_ATOL)
+    np.testing.assert_allclose([ep[0][k] for k in EPKEYS], z["resets_info"][0], rtol=1e-12, atol=1e-12)
+    n_reset = 1
+    c_mr, c_sf, c_dec = _info_col("min_relative_distance"), _info_col("Safety filtered"), \
+        _info_col("deconflicting_agent_index")
+    c_rg = _info_col("reached_goal")
+    for t in range(meta["steps"]):
+        ctx = "%s step %d" % (name, t)
+        obs, aid, node, adj, rew, dones, infos = env.step(z["act"][t][None], meta["ep"])
+        info = env.t_info.cpu().numpy()[0]
+        reset = bool(env.t_reset.cpu().numpy()[0])
+        np.testing.assert_array_equal(dones[0], z["dones"][t], err_msg=ctx)
+        np.testing.assert_allclose(rew[0], z["rew"][t], rtol=1e-6, atol=1e-5, err_msg=ctx)
+        np.testing.assert_array_equal(info[:, c_rg], z["reached"][t], err_msg=ctx)
+        np.testing.assert_allclose(info[:, c_mr], z["minrel"][t], rtol=1e-12, atol=1e-12, err_msg=ctx)
+        np.testing.assert_array_equal(info[:, c_sf].astype(bool), z["sfilt"][t], err_msg=ctx)
+        np.testing.assert_array_equal(info[:, c_dec].astype(int), z["decon"][t], err_msg=ctx)
+        ref_info = z["info_num"][t]
+        for j, k in enumerate(INFOKEYS):
+            np.testing.assert_allclose(info[:, _info_col(k)], ref_info[:, j], rtol=1e-9, atol=1e-9,
+                                       err_msg=ctx + " info " + k)
+        if not reset:
+            np.testing.assert_allclose(env.state().cpu().numpy()[0], z["state"][t], rtol=0, atol=STATE_ATOL,
+                                       err_msg=ctx)
+            np.testing.assert_allclose(obs[0], z["obs"][t], rtol=0, atol=F32_ATOL, err_msg=ctx)
+            np.testing.assert_array_equal(adj_bits(adj[0]), z["adj_bits"][t], err_msg=ctx)
+            key = "t%03d_node" % t
+            if key in z.files:
+                np.testing.assert_allclose(node[0], z[key], rtol=0, atol=F32_ATOL, err_msg=ctx)
+                np.testing.assert_allclose(adj[0], z["t%03d_adj" % t], rtol=0, atol=F32_ATOL, err_msg=ctx)
+                e = np.stack(np.nonzero(env.t_edges.cpu().numpy()[0]))
+                np.testing.assert_array_equal(e, z["t%03d_edges" % t], err_msg=ctx)
+        else:
+            assert z["resets_t"][n_reset] == t + 1, ctx
+            assert len(infos[0]) == meta["num_agents"] + 1
+            np.testing.assert_allclose([infos[0][-1][k] for k in EPKEYS], z["resets_info"][n_reset],
+                                       rtol=1e-9, atol=1e-9, err_msg=ctx)
+            np.testing.assert_allclose(env.state().cpu().numpy()[0], z["t%03d_reset_state" % t],
+                                       rtol=0, atol=STATE_ATOL, err_msg=ctx)
+            np.testing.assert_allclose(obs[0], z["t%03d_reset_obs" % t], rtol=0, atol=F32_ATOL, err_msg=ctx)
+            np.testing.assert_allclose(node[0], z["t%03d_reset_node" % t], rtol=0, atol=F32_ATOL, err_msg=ctx)
+            np.testing.assert_allclose(adj[0], z["t%03d_reset_adj" % t], rtol=0, atol=F32_ATOL, err_msg=ctx)
+            n_reset += 1
+    assert n_reset == len(z["resets_t"])
+    env.close()
+
+
+def _oracle_for(meta, seed, n_envs, env_offset=0):
+    from oracle.lsm_oracle import OracleVecEnv
+    vt, tt = tables_for(meta)
+    return OracleVecEnv(meta, n_envs, seed=seed, value_table=table_dict(vt), ttr_table=table_dict(tt),
+                        integrator="closed", seed_offset=env_offset)
+
+
+CASES = [
+    dict(dynamics_type="double_integrator", num_agents=8, world_size=4, episode_length=250,
+         num_env_steps=250 * 4, use_safety_filter=True, ep=4),
+    dict(dynamics_type="double_integrator", num_agents=8, world_size=4, episode_length=250,
+         num_env_steps=250 * 4, use_safety_filter=False, ep=1),
+    dict(dynamics_type="double_integrator", num_agents=5, world_size=4, episode_length=60,
+         num_env_steps=60 * 4, use_safety_filter=True, ep=3),
+    dict(dynamics_type="airtaxi", num_agents=6, world_size=6, episode_length=80,
+         num_env_steps=80 * 4, use_safety_filter=True, ep=4),
+    dict(dynamics_type="airtaxi", num_agents=4, world_size=6, episode_length=80,
+         num_env_steps=80 * 4, use_safety_filter=False, ep=2),
+]
+
+
+@pytest.mark.parametrize("case", range(len(CASES)))
+def test_gpu_matches_oracle_multi_env(case):
+    """16 envs with per-env seeds seed + 1000 k, random actions, across an auto-reset."""
+    c = dict(CASES[case])
+    ep = c.pop("ep")
+    meta = dict(num_landmarks=2, n_rollout_threads=1, use_masking=True, num_internal_step=1, seed=5,
+                env_seed=5, **c)
+    n_envs, steps = 16, min(c["episode_length"] + 20, 120)
+    env = _gpu_env(meta, n_envs=n_envs, seed=5)
+    ora = _oracle_for(meta, 5, n_envs)
+    g = env.reset(ep)
+    o = ora.reset(ep)
+    np.testing.assert_allclose(g[0], o[0], rtol=0, atol=F32_ATOL)
+    np.testing.assert_allclose(g[2], o[2], rtol=0, atol=F32_ATOL)
+    np.testing.assert_array_equal(g[3] != 0, o[3] != 0)
+    rng = np.random.default_rng(case)
+    mism = 0
+    for t in range(steps):
+        a = rng.integers(0, 25, (n_envs, meta["num_agents"]))
+        g = env.step(a, ep)
+        o = ora.step(a, ep)
+        ctx = "case %d step %d" % (case, t)
+        np.testing.assert_array_equal(g[5], o[5], err_msg=ctx)
+        np.testing.assert_array_equal(g[3] != 0, o[3] != 0, err_msg=ctx)
+        np.testing.assert_allclose(g[0], o[0], rtol=0, atol=F32_ATOL, err_msg=ctx)
+        np.testing.assert_allclose(g[2], o[2], rtol=0, atol=F32_ATOL, err_msg=ctx)
+        np.testing.assert_allclose(g[3], o[3], rtol=0, atol=F32_ATOL, err_msg=ctx)
+        np.testing.assert_allclose(g[4], o[4], rtol=1e-6, atol=1e-5, err_msg=ctx)
+        st = env.state().cpu().numpy()
+        for k, e in enumerate(ora.envs):
+            np.testing.assert_allclose(st[k], e.s, rtol=0, atol=STATE_ATOL, err_msg=ctx)
+            mism += int(np.any(st[k] != e.s))
+    env.close()
+
+
+def test_gpu_full_size_properties_and_sampled_oracle():
+    """BASELINE config 3 size (8 agents x 4096 envs, filter on): invariants over 260 steps
+    (one auto-reset at step 250) + exact replay of sampled envs through the oracle."""
+    import torch
+    meta = dict(dynamics_type="double_integrator", num_agents=8, num_landmarks=2, world_size=4,
+                episode_length=250, num_env_steps=250 * 4, n_rollout_threads=1, use_safety_filter=True,
+                use_masking=True, num_internal_step=1, seed=0, env_seed=0)
+    n_envs = 4096
+    env = _gpu_env(meta, n_envs=n_envs, seed=0, return_numpy=False)
+    sample = [0, 1, 1337, 4095]
+    oras = [_oracle_for(meta, 0, 1, env_offset=k) for k in sample]
+    obs, aid, node, adj, ep = env.reset(4)
+    for k, o in zip(sample, oras):
+        r = o.reset(4)
+        np.testing.assert_allclose(obs[k].cpu().numpy(), r[0][0], rtol=0, atol=F32_ATOL)
+    gen = torch.Generator(device="cuda:0").manual_seed(0)
+    N = 8
+    for t in range(260):
+        a = torch.randint(0, 25, (n_envs, N), device="cuda:0", generator=gen, dtype=torch.int32)
+        obs, aid, node, adj, rew, dones, (info, reset, epinfo) = env.step(a, 4)
+        a_h = a.cpu().numpy()
+        st = env.state()
+        if t % 20 == 0 or t >= 248:
+            assert torch.isfinite(obs).all() and torch.isfinite(node).all() and torch.isfinite(adj).all()
+            assert (adj >= 0).all() and (adj < 4).all()
+            d = torch.diagonal(adj, dim1=2, dim2=3)
+            assert (d == 0).all()
+            assert torch.equal(adj, adj.transpose(2, 3))
+            sp = torch.sqrt(st[..., 2] ** 2 + st[..., 3] ** 2)
+            assert (sp <= 0.5 + 1e-12).all()
+        if t == 249:
+            assert bool(reset.all())
+        elif t < 249:
+            assert not bool(reset.any()) or bool(dones.all(dim=1)[reset.bool()].all())
+        for k, o in zip(sample, oras):
+            r = o.step(a_h[k:k + 1], 4)
+            np.testing.assert_array_equal(dones[k].cpu().numpy(), r[5][0], err_msg="env %d step %d" % (k, t))
+            np.testing.assert_array_equal((adj[k] != 0).cpu().numpy(), r[3][0] != 0)
+            np.testing.assert_allclose(obs[k].cpu().numpy(), r[0][0], rtol=0, atol=F32_ATOL)
+            np.testing.assert_allclose(st[k].cpu().numpy(), o.envs[0].s, rtol=0, atol=STATE_ATOL)
+    env.close()
