@@ -53,7 +53,7 @@ def test_gpu_matches_reference_golden(name):
         np.testing.assert_array_equal(dones[0], z["dones"][t], err_msg=ctx)
         np.testing.assert_allclose(rew[0], z["rew"][t], rtol=1e-6, atol=1e-5, err_msg=ctx)
         np.testing.assert_array_equal(info[:, c_rg], z["reached"][t], err_msg=ctx)
-        np.testing.assert_allclose(info[:, c_mr], z["minrel"][t], rtol=1e-12, atol=1e-12, err_msg=ctx)
+        np.testing.assert_allclose(info[:, c_mr], z["minrel"][t], rtol=0, atol=STATE_ATOL, err_msg=ctx)
         np.testing.assert_array_equal(info[:, c_sf].astype(bool), z["sfilt"][t], err_msg=ctx)
         np.testing.assert_array_equal(info[:, c_dec].astype(int), z["decon"][t], err_msg=ctx)
         ref_info = z["info_num"][t]
