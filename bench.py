@@ -1,0 +1,212 @@
+#!/usr/bin/env python
+"""Benchmark: agent-env-steps/s of the navigation_graph_safe rollout on MI355X.
+
+A "step" = one vec-env step (one rollout_kernel launch) over this GPU's batch of
+envs, including device auto-resets at episode ends, with actions drawn on device.
+Default workload = BASELINE.json configs[2] (the headline metric's config): double
+integrator, 8 agents x 4096 envs per GPU, HJ safety filter on, reference output
+layout (per-ego node_obs / adjacency). Multi-GPU: one process per GPU (torchrun),
+envs sharded by global index (weak scaling), RCCL all_reduce of the episode
+summary at each episode boundary, max-over-ranks timing.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import multiprocessing as mp
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "layered-safe-marl_amd"))
+
+METRIC = "agent-env-steps/sec at 8 agents × 4096 envs, safety filter on; 1/2/4/8 GPU"
+PEAK_HBM_GBPS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+CONFIGS = {
+    2: dict(workload="8-agent double-integrator, 4096 envs per GPU, safety filter off",
+            dynamics_type="double_integrator", num_agents=8, envs=4096, use_safety_filter=False,
+            world_size=4, episode_length=250),
+    3: dict(workload="8-agent double-integrator, 4096 envs per GPU, HJ safety filter on",
+            dynamics_type="double_integrator", num_agents=8, envs=4096, use_safety_filter=True,
+            world_size=4, episode_length=250),
+    4: dict(workload="16-agent airtaxi (Dubins), 8192 envs per GPU, HJ safety filter on",
+            dynamics_type="airtaxi", num_agents=16, envs=8192, use_safety_filter=True,
+            world_size=6, episode_length=350),
+}
+
+
+def make_args(c, seed=0):
+    from lsm.config import EnvArgs
+    return EnvArgs(dynamics_type=c["dynamics_type"], num_agents=c["num_agents"], num_landmarks=2,
+                   world_size=c["world_size"], episode_length=c["episode_length"],
+                   num_env_steps=c["episode_length"] * 4, n_rollout_threads=1,
+                   use_safety_filter=c["use_safety_filter"], seed=seed)
+
+
+# ---- CPU baseline: the oracle ("port") on the host cores, bounded sample --------------------
+_CPU_CTX = {}
+
+
+def _cpu_worker(k):
+    from oracle.lsm_oracle import OracleVecEnv
+    import numpy as np
+    c = _CPU_CTX
+    ora = OracleVecEnv(vars(c["args"]), c["envs_per_worker"], seed=0, value_table=c["vt"], ttr_table=c["tt"],
+                       integrator="rk45", seed_offset=k * c["envs_per_worker"])
+    ora.reset(c["ep"])
+    rng = np.random.default_rng(1 + k)
+    N = c["args"].num_agents
+    t0 = time.perf_counter()
+    for _ in range(c["steps"]):
+        ora.step(rng.integers(0, 25, (c["envs_per_worker"], N)), c["ep"])
+    return time.perf_counter() - t0
+
+
+def cpu_baseline(args, vt, tt, ep, cores, envs_per_worker=2, steps=60):
+    _CPU_CTX.update(args=args, vt=vt, tt=tt, ep=ep, envs_per_worker=envs_per_worker, steps=steps)
+    ctx = mp.get_context("fork")
+    with ctx.Pool(cores) as pool:
+        times = pool.map(_cpu_worker, range(cores))
+    agent_steps = cores * envs_per_worker * steps * args.num_agents
+    return dict(value=agent_steps / max(times), unit="agent-steps/s", cores=cores, kind="port",
+                sample="oracle/lsm_oracle.py (reference semantics, scipy RK45), %d worker processes x %d envs x "
+                       "%d steps, N=%d, filter %s, full-size synthetic HJ table; wall %.1f s"
+                       % (cores, envs_per_worker, steps, args.num_agents,
+                          "on" if args.use_safety_filter else "off", max(times)))
+
+
+def table_dict(t):
+    if t is None:
+        return None
+    return dict(lo=t.lo, hi=t.hi, shape=t.shape, periodic=t.periodic, values_hj=t.values_hj,
+                grads_hj=t.grads_hj, separation_distance=t.separation_distance, values=t.values_hj,
+                ttr_max=t.ttr_max)
+
+
+def load_traffic(config, n_envs):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary of the same workload."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        d = json.load(open(p))
+        e = d.get(str(config))
+        if e and int(e.get("num_envs", -1)) == n_envs:
+            return float(e["hbm_bytes_per_launch"])
+    except Exception:
+        return None
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=1000)
+    ap.add_argument("--warmup", type=int, default=250)
+    ap.add_argument("--config", type=int, default=3, choices=sorted(CONFIGS))
+    ap.add_argument("--envs", type=int, default=0, help="envs per GPU (default: config's)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-cores", type=int, default=0)
+    a = ap.parse_args()
+
+    from lsm.dist import rank_info, global_episode_summary
+    rank, world, local_rank = rank_info()
+    c = CONFIGS[a.config]
+    n_envs = a.envs or c["envs"]
+    args = make_args(c)
+    from lsm import hj_tables
+    vt, tt = (hj_tables.default_tables(c["dynamics_type"]) if (c["use_safety_filter"] or
+              c["dynamics_type"] != "double_integrator") else (None, None))
+    ep = 4  # curriculum ratio 1: the filter is active when requested (SURVEY finding 5)
+
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        cores = a.cpu_cores or min(16, len(os.sched_getaffinity(0)))
+        cpu = cpu_baseline(args, table_dict(vt), table_dict(tt), ep, cores)
+
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        dist.init_process_group("nccl")
+    dev = torch.device("cuda:%d" % local_rank)
+    torch.cuda.set_device(dev)
+    from lsm.vec_env import GpuGraphVecEnv
+    env = GpuGraphVecEnv(args, num_envs=n_envs, device=dev, value_table=vt, ttr_table=tt,
+                         env_offset=rank * n_envs, return_numpy=False, build_infos=False)
+    N = c["num_agents"]
+    gen = torch.Generator(device=dev).manual_seed(1234 + rank)
+    acts = torch.empty((n_envs, N), dtype=torch.int32, device=dev)
+    env.reset(ep)
+    epl = c["episode_length"]
+
+    def one_step(t, ev=None):
+        torch.randint(0, 25, (n_envs, N), generator=gen, device=dev, dtype=torch.int32, out=acts)
+        if ev is not None:
+            ev[0].record()
+        env.step_async(acts, ep)
+        if ev is not None:
+            ev[1].record()
+        env.step_wait()
+        if (t + 1) % epl == 0:   # episode boundary: RCCL reduction of the episode summary
+            global_episode_summary(env.t_epinfo)
+
+    for t in range(a.warmup):
+        one_step(t)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for t in range(a.steps):
+        one_step(a.warmup + t, evs[t])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kern_ms = sum(e0.elapsed_time(e1) for e0, e1 in evs) / a.steps
+    if world > 1:
+        tt_ = torch.tensor([elapsed, kern_ms], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt_, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms = tt_.tolist()
+    total_agent_steps = world * n_envs * N * a.steps
+    value = total_agent_steps / elapsed
+    from lsm.perf_model import step_bytes
+    sb = step_bytes(N, 2, c["dynamics_type"], c["use_safety_filter"])
+    bytes_launch = sb["hbm_bytes"] * n_envs
+    achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
+    traffic = load_traffic(a.config, n_envs)
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": value, "unit": "agent-steps/s", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": elapsed * 1e3 / a.steps, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+            "config": {"workload": c["workload"], "num_agents": N, "envs_per_gpu": n_envs,
+                       "total_envs": world * n_envs, "dynamics": c["dynamics_type"],
+                       "safety_filter": c["use_safety_filter"], "episode_length": epl,
+                       "output_layout": "reference (per-ego node_obs/adj, fp32)",
+                       "hj_table": "synthetic %s" % (vt.shape if vt is not None else None),
+                       "parallelism": "env-sharded dp%d" % world},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
+                         "frac": achieved / PEAK_HBM_GBPS, "traffic": traffic,
+                         "kernel": "rollout_kernel<%d>" % (0 if c["dynamics_type"] == "double_integrator" else 1),
+                         "kernel_ms": kern_ms, "algorithmic_bytes_per_launch": bytes_launch,
+                         "gather_bytes_per_launch": sb["gather_bytes"] * n_envs},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    env.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

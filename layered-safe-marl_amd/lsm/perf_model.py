@@ -1,0 +1,37 @@
+"""Algorithmic HBM bytes of one ``rollout_kernel`` launch (the bench's roofline numerator).
+
+Counts the bytes that MUST cross HBM for one env-step of the reference-layout
+path, per env:
+
+* state read + written back: agent state 4N f64, travel distance N f64, done N u8,
+  reached_goal N i32, landmarks 4NL f64 (read; written back), step counter i32,
+  curriculum block 12 f64 (read), episode stats 6N f64, info accumulators 4N f64,
+  goal_min_time N f64 (read), safety flags / indices / min distance / action diff
+  (N u8 + N i32 + 2N f64, written);
+* actions: N i32 read;
+* outputs written: obs N*OBS f32, node_obs N*E*F f32, adj N*E*E f32, reward N f32,
+  done N u8, reset flag 1 u8, info N*16 f64, state copy 4N f64.
+
+HJ-table gathers (16 or 32 corners per pair) are served from the 256 MiB
+Infinity Cache / L2 for the 125 MB full-size table and are reported separately
+as ``gather_bytes`` -- they are not HBM-algorithmic bytes.
+"""
+from __future__ import annotations
+
+
+def step_bytes(N: int, L: int = 2, dynamics: str = "double_integrator", filter_on: bool = True) -> dict:
+    NL = N * L
+    E = N + NL
+    di = dynamics == "double_integrator"
+    F = 10 if di else 11
+    OBS = 7 if di else 6
+    state_rw = 2 * (4 * N * 8 + N * 8 + N + N * 4 + 4 * NL * 8 + 4 + 6 * N * 8 + 4 * N * 8)
+    state_r = 12 * 8 + N * 8 + N * 4
+    state_w = N + N * 4 + 2 * N * 8
+    outputs = N * OBS * 4 + N * E * F * 4 + N * E * E * 4 + N * 4 + N + 1 + N * 16 * 8 + 4 * N * 8
+    hbm = state_rw + state_r + state_w + outputs
+    corners = 16 if di else 32
+    gw = 16 if di else 32
+    gathers = (corners * 4 * N * (N - 1) + corners * gw * N) if filter_on else 0
+    return dict(hbm_bytes=hbm, outputs=outputs, state=state_rw + state_r + state_w, gather_bytes=gathers,
+                E=E, F=F, OBS=OBS)

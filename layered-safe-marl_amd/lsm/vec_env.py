@@ -126,6 +126,7 @@ class GpuGraphVecEnv:
         self.agent_id_observation_space = [Box(-np.inf, np.inf, (1,)) for _ in range(N)]
         self.share_agent_id_observation_space = [Box(-np.inf, np.inf, (N,)) for _ in range(N)]
         self._pending = None
+        self._cur_cache = {}
         self._last_ep = 0
         self._sep_tracked = None
         self.closed = False
@@ -192,11 +193,17 @@ class GpuGraphVecEnv:
             return t.to(torch.float32).contiguous(), capi.LSM_ACTIONS_ONEHOT_F32
         raise ValueError("actions must be (n_envs, N) indices or (n_envs, N, 25) one-hot")
 
+    def _curriculum(self, ep):
+        c = self._cur_cache.get(ep)
+        if c is None:
+            block = curriculum_block(self.args, ep)
+            c = self._cur_cache[ep] = (block, to_struct(block))
+        return c
+
     def step_async(self, actions, num_current_episode: Optional[int] = None):
         ep = self._last_ep if num_current_episode is None else num_current_episode
-        block = curriculum_block(self.args, ep)
+        block, cur = self._curriculum(ep)
         act, kind = self._actions_device(actions)
-        cur = to_struct(block)
         capi.check(self.lib.lsm_step(self.h, C.c_void_p(act.data_ptr()), kind, C.byref(cur), self._stream()),
                    self.h)
         self._pending = (act, block)
