@@ -68,7 +68,7 @@ def _cpu_worker(k):
     return time.perf_counter() - t0
 
 
-def cpu_baseline(args, vt, tt, ep, cores, envs_per_worker=2, steps=60):
+def cpu_baseline(args, vt, tt, ep, cores, envs_per_worker=4, steps=250):
     _CPU_CTX.update(args=args, vt=vt, tt=tt, ep=ep, envs_per_worker=envs_per_worker, steps=steps)
     ctx = mp.get_context("fork")
     with ctx.Pool(cores) as pool:
@@ -193,7 +193,7 @@ def main():
                        "total_envs": world * n_envs, "dynamics": c["dynamics_type"],
                        "safety_filter": c["use_safety_filter"], "episode_length": epl,
                        "output_layout": "reference (per-ego node_obs/adj, fp32)",
-                       "hj_table": "synthetic %s" % (vt.shape if vt is not None else None),
+                       "hj_table": "synthetic %s" % (str(vt.shape) if vt is not None else "none"),
                        "parallelism": "env-sharded dp%d" % world},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
                          "frac": achieved / PEAK_HBM_GBPS, "traffic": traffic,
