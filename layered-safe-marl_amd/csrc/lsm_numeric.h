@@ -43,35 +43,45 @@ LSM_HD void blas_rot(double c, double s, double vx, double vy, double& ox, doubl
   oy = fma(-s, vx, c * vy);
 }
 
-// numpy pairwise summation (pairwise_sum_DOUBLE) for n <= 128 (recursion beyond).
-LSM_HD double np_sum(const double* a, int n) {
+// numpy pairwise summation (pairwise_sum_DOUBLE), n <= 128 (the path never sums more),
+// over an accessor so device code needs no private arrays.
+template <class A>
+LSM_HD double np_sum_acc(const A& a, int n) {
   if (n < 8) {
     double res = 0.0;
-    for (int i = 0; i < n; ++i) res += a[i];
+    for (int i = 0; i < n; ++i) res += a(i);
     return res;
   }
-  if (n <= 128) {
-    double r[8];
-    for (int j = 0; j < 8; ++j) r[j] = a[j];
-    int i = 8;
-    for (; i < n - (n % 8); i += 8)
-      for (int j = 0; j < 8; ++j) r[j] += a[i + j];
-    double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
-    for (; i < n; ++i) res += a[i];
-    return res;
+  double r0 = a(0), r1 = a(1), r2 = a(2), r3 = a(3), r4 = a(4), r5 = a(5), r6 = a(6), r7 = a(7);
+  int i = 8;
+  for (; i < n - (n % 8); i += 8) {
+    r0 += a(i); r1 += a(i + 1); r2 += a(i + 2); r3 += a(i + 3);
+    r4 += a(i + 4); r5 += a(i + 5); r6 += a(i + 6); r7 += a(i + 7);
   }
-  int n2 = n / 2;
-  n2 -= n2 % 8;
-  return np_sum(a, n2) + np_sum(a + n2, n - n2);
+  double res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
+  for (; i < n; ++i) res += a(i);
+  return res;
 }
+struct ArrAcc {
+  const double* p;
+  LSM_HD double operator()(int i) const { return p[i]; }
+};
+LSM_HD double np_sum(const double* a, int n) { return np_sum_acc(ArrAcc{a}, n); }
 LSM_HD double np_mean(const double* a, int n) { return np_sum(a, n) / (double)n; }
-LSM_HD double np_std(const double* a, int n, double* scratch) {
-  double m = np_mean(a, n);
-  for (int i = 0; i < n; ++i) {
-    double d = a[i] - m;
-    scratch[i] = d * d;
+template <class A>
+struct SqDevAcc {
+  A a;
+  double m;
+  LSM_HD double operator()(int i) const {
+    const double d = a(i) - m;
+    return d * d;
   }
-  return sqrt(np_sum(scratch, n) / (double)n);
+};
+// np.mean / np.std of an accessor-defined array (np.std: sqrt(mean(|x - mean|^2)))
+template <class A>
+LSM_HD void np_mean_std(const A& a, int n, double& mean, double& std) {
+  mean = np_sum_acc(a, n) / (double)n;
+  std = sqrt(np_sum_acc(SqDevAcc<A>{a, mean}, n) / (double)n);
 }
 
 // direction_alignment_error (custom_scenarios/utils.py:79-81).

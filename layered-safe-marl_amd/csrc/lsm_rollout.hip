@@ -101,6 +101,7 @@ struct KParams {
   float at_box_w, at_box_amax, at_box_amin;  // float32 box corners (jnp)
   double ttr_max;
   double cur_new[NCUR];
+  uint32_t m_E, m_EE, m_EF, m_F;  // ceil(2^32 / d) for exact small-numerator division
   TableDev val, ttr;
   StateDev s;
   OutDev o;
@@ -130,7 +131,14 @@ struct Lds {
   float* stage;      // [64][F]
   uint32_t* mt;      // [MT_WORDS]
   double* cur;       // [NCUR]
+  uint64_t* emask;   // [N] bit r: entity r disconnected for ego e (snapshot rule)
+  double* feat;      // [2][E][F] DI entity rows (version 0 = pre, 1 = post reward update)
+  double* egooff;    // [N][F]   DI ego offsets subtracted from the entity rows
+  double* scen;      // [SCEN_WS] scenario workspace
 };
+
+// q / d for q * d < 2^32 (all index math here): __umulhi(q, ceil(2^32 / d))
+__device__ __forceinline__ int fdiv(int q, uint32_t m) { return (int)__umulhi((uint32_t)q, m); }
 
 __host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
 
@@ -150,10 +158,14 @@ __host__ __device__ inline size_t lds_bytes(int N, int NL, int E, int F) {
   b += align16(sizeof(float) * 64 * F);
   b += align16(sizeof(uint32_t) * MT_WORDS);
   b += align16(sizeof(double) * NCUR);
+  b += align16(sizeof(uint64_t) * N);
+  b += align16(sizeof(double) * 2 * E * F);
+  b += align16(sizeof(double) * N * F);
+  b += align16(sizeof(double) * SCEN_WS);
   return b;
 }
 
-__device__ inline Lds carve(unsigned char* base, int N, int NL, int E, int F) {
+__device__ __forceinline__ Lds carve(unsigned char* base, int N, int NL, int E, int F) {
   Lds L;
   size_t o = 0;
   auto take = [&](size_t bytes) { unsigned char* p = base + o; o += align16(bytes); return p; };
@@ -176,6 +188,10 @@ __device__ inline Lds carve(unsigned char* base, int N, int NL, int E, int F) {
   L.stage = (float*)take(sizeof(float) * 64 * F);
   L.mt = (uint32_t*)take(sizeof(uint32_t) * MT_WORDS);
   L.cur = (double*)take(sizeof(double) * NCUR);
+  L.emask = (uint64_t*)take(sizeof(uint64_t) * N);
+  L.feat = (double*)take(sizeof(double) * 2 * E * F);
+  L.egooff = (double*)take(sizeof(double) * N * F);
+  L.scen = (double*)take(sizeof(double) * SCEN_WS);
   return L;
 }
 
@@ -187,7 +203,7 @@ enum { C_CR = 0, C_SLOPED, C_STAIR, C_RAT, C_RSC, C_GHE, C_GSE, C_MDT, C_SEP, C_
 struct WaveRng {
   uint32_t* key;
   int pos;
-  __device__ void gen() {
+  __device__ __forceinline__ void gen() {
     const int lane = threadIdx.x;
     // phase A: i in [0, 227) reads old key[i], key[i+1], key[i+397]
     for (int base = 0; base < MT_N - MT_M; base += WAVE) {
@@ -211,18 +227,18 @@ struct WaveRng {
     __syncthreads();
     pos = 0;
   }
-  __device__ uint32_t next32() {
+  __device__ __forceinline__ uint32_t next32() {
     if (pos >= MT_N) gen();
     uint32_t y = key[pos];
     pos++;
     return mt_temper(y);
   }
-  __device__ double next_double() {
+  __device__ __forceinline__ double next_double() {
     uint32_t a = next32() >> 5;
     uint32_t b = next32() >> 6;
     return (a * 67108864.0 + b) / 9007199254740992.0;
   }
-  __device__ double uniform(double lo, double hi) {
+  __device__ __forceinline__ double uniform(double lo, double hi) {
     double range = hi - lo;
     return lo + range * next_double();
   }
@@ -232,7 +248,7 @@ struct WaveRng {
 // HJ grid interpolation (float32; semantics of oracle/hj_grid.py)
 // ----------------------------------------------------------------------------------
 template <int ND>
-__device__ inline bool grid_corners(const TableDev& T, const double* s, int* off, float* w) {
+__device__ __forceinline__ bool grid_corners(const TableDev& T, const double* s, int* off, float* w) {
   float wl[ND], wh[ND];
   int il[ND], ih[ND];
 #pragma unroll
@@ -278,7 +294,7 @@ __device__ inline bool grid_corners(const TableDev& T, const double* s, int* off
 }
 
 template <int ND>
-__device__ inline bool interp_value(const TableDev& T, const double* s, float& out) {
+__device__ __forceinline__ bool interp_value(const TableDev& T, const double* s, float& out) {
   int off[1 << ND];
   float w[1 << ND];
   if (!grid_corners<ND>(T, s, off, w)) return false;
@@ -293,7 +309,7 @@ __device__ inline bool interp_value(const TableDev& T, const double* s, float& o
 }
 
 template <int ND>
-__device__ inline void interp_grad(const TableDev& T, const double* s, float* g) {
+__device__ __forceinline__ void interp_grad(const TableDev& T, const double* s, float* g) {
   int off[1 << ND];
   float w[1 << ND];
   for (int d = 0; d < ND; ++d) g[d] = 0.0f;
@@ -317,7 +333,7 @@ __device__ inline void interp_grad(const TableDev& T, const double* s, float* g)
 // ----------------------------------------------------------------------------------
 // per-agent helpers
 // ----------------------------------------------------------------------------------
-__device__ inline int goal_index(int reached, int j, int N, int NL) {
+__device__ __forceinline__ int goal_index(int reached, int j, int N, int NL) {
   int order = reached * N + j;
   if (order >= NL) order = (reached - 1) * N + j;
   // the reference raises past the last landmark (use_masking=False only); clamp for safety
@@ -327,7 +343,7 @@ __device__ inline int goal_index(int reached, int j, int N, int NL) {
 
 // agent j velocity components for a given "post" choice.
 template <int DYN>
-__device__ inline void agent_vel(const Lds& S, int N, int j, bool post, double& vx, double& vy) {
+__device__ __forceinline__ void agent_vel(const Lds& S, int N, int j, bool post, double& vx, double& vy) {
   const bool frozen = post && S.dpost[j];
   if (DYN == 0) {
     vx = frozen ? 0.0 : S.ps[2 * N + j];
@@ -341,7 +357,7 @@ __device__ inline void agent_vel(const Lds& S, int N, int j, bool post, double& 
 }
 
 template <int DYN>
-__device__ inline double agent_speed(const Lds& S, int N, int j, bool post) {
+__device__ __forceinline__ double agent_speed(const Lds& S, int N, int j, bool post) {
   const bool frozen = post && S.dpost[j];
   if (DYN == 0) {
     const double vx = frozen ? 0.0 : S.ps[2 * N + j];
@@ -352,7 +368,7 @@ __device__ inline double agent_speed(const Lds& S, int N, int j, bool post) {
 }
 
 template <int DYN>
-__device__ inline double agent_theta(const Lds& S, int N, int j, bool post) {
+__device__ __forceinline__ double agent_theta(const Lds& S, int N, int j, bool post) {
   if (DYN == 0) {
     const bool frozen = post && S.dpost[j];
     const double vx = frozen ? 0.0 : S.ps[2 * N + j];
@@ -364,7 +380,7 @@ __device__ inline double agent_theta(const Lds& S, int N, int j, bool post) {
 
 // evaluate_agent_goal_reached (navigation_graph_safe.py:606-656)
 template <int DYN>
-__device__ inline bool goal_reached(const KParams& P, const Lds& S, int i, bool post, int reached) {
+__device__ __forceinline__ bool goal_reached(const KParams& P, const Lds& S, int i, bool post, int reached) {
   const int N = P.N, NL = P.NL;
   const int gi = goal_index(reached, i, N, NL);
   const double gx = S.lm[gi], gy = S.lm[NL + gi], gh = S.lm[2 * NL + gi], gs = S.lm[3 * NL + gi];
@@ -395,7 +411,7 @@ __device__ inline bool goal_reached(const KParams& P, const Lds& S, int i, bool 
 }
 
 // double_integrator_velocity_error_from_magnetic_field_reference (utils.py:276-349)
-__device__ inline double magnetic_penalty(const KParams& P, double px, double py, double vx, double vy,
+__device__ __forceinline__ double magnetic_penalty(const KParams& P, double px, double py, double vx, double vy,
                                           double gx, double gy, double gh, double gs, double radius) {
   const double ch = cos(gh), sh = sin(gh);
   double rpx, rpy, rvx, rvy;
@@ -432,7 +448,7 @@ __device__ inline double magnetic_penalty(const KParams& P, double px, double py
   return err * (1 - ar) + dist * ar;
 }
 
-__device__ inline double seqdot4(const double* a, const double* b) {
+__device__ __forceinline__ double seqdot4(const double* a, const double* b) {
   double acc = 0.0;
   for (int k = 0; k < 4; ++k) acc = acc + a[k] * b[k];
   return acc;
@@ -442,7 +458,7 @@ __device__ inline double seqdot4(const double* a, const double* b) {
 // safety filter for one ego (lane), after pair scratch is filled
 // ----------------------------------------------------------------------------------
 template <int DYN>
-__device__ inline void rel_state(const Lds& S, int N, int e, int o, double* rel) {
+__device__ __forceinline__ void rel_state(const Lds& S, int N, int e, int o, double* rel) {
   const double ex = S.ps[e], ey = S.ps[N + e], e2 = S.ps[2 * N + e], e3 = S.ps[3 * N + e];
   const double ox = S.ps[o], oy = S.ps[N + o], o2 = S.ps[2 * N + o], o3 = S.ps[3 * N + o];
   if (DYN == 0) {
@@ -460,7 +476,7 @@ __device__ inline void rel_state(const Lds& S, int N, int e, int o, double* rel)
 }
 
 template <int DYN>
-__device__ inline void filter_ego(const KParams& P, Lds& S, int i, uint8_t& filtered, int& dec,
+__device__ __forceinline__ void filter_ego(const KParams& P, Lds& S, int i, uint8_t& filtered, int& dec,
                                   double& u0, double& u1) {
   const int N = P.N;
   u0 = S.raw[i];
@@ -608,7 +624,7 @@ __device__ inline void filter_ego(const KParams& P, Lds& S, int i, uint8_t& filt
 // ego i sees agent j "post" (after its reward update) iff j <= i.
 // ----------------------------------------------------------------------------------
 template <int DYN>
-__device__ inline void node_features(const KParams& P, const Lds& S, int e, int k, float* f) {
+__device__ __forceinline__ void node_features(const KParams& P, const Lds& S, int e, int k, float* f) {
   const int N = P.N, NL = P.NL;
   const double pex = S.ps[e], pey = S.ps[N + e];
   double vex, vey;
@@ -689,55 +705,134 @@ __device__ inline void node_features(const KParams& P, const Lds& S, int e, int 
   }
 }
 
-// entity r masked for ego e (snapshot)
-__device__ inline bool masked(const Lds& S, int N, int e, int r) {
-  if (r < N) return (r <= e) ? S.dpost[r] != 0 : S.dpre[r] != 0;
-  const int l = r - N;
-  const int a = l % N, order = l / N;
-  const int rg = (a <= e) ? S.rpost[a] : S.rpre[a];
-  return rg > order;
+// Disconnect mask of ego e (navigation_graph_safe.py:976-989) under the sequential snapshot
+// rule: agent j is seen after its reward update iff j <= e. Bit r = entity r (agents first,
+// landmark l = order * N + agent at N + l). e >= N - 1 gives the end-of-step mask.
+__device__ __forceinline__ uint64_t ego_mask(const Lds& S, int N, int L, int e) {
+  uint64_t m = 0;
+  for (int j = 0; j < N; ++j) {
+    const bool post = j <= e;
+    if (post ? S.dpost[j] : S.dpre[j]) m |= 1ull << j;
+    const int rg = post ? S.rpost[j] : S.rpre[j];
+    for (int o = 0; o < L; ++o)
+      if (rg > o) m |= 1ull << (N + o * N + j);
+  }
+  return m;
+}
+
+// DI node features are (entity row) - (ego offset): build both once per step in LDS.
+__device__ __forceinline__ void build_rows_di(const KParams& P, Lds& S) {
+  const int lane = threadIdx.x;
+  const int N = P.N, NL = P.NL, E = P.E, F = P.F;
+  for (int t = lane; t < 2 * E; t += WAVE) {
+    const int v = t >= E ? 1 : 0;
+    const int k = t - v * E;
+    double* r = S.feat + (size_t)(v * E + k) * F;
+    if (k < N) {
+      const bool post = v == 1;
+      double vx, vy;
+      agent_vel<0>(S, N, k, post, vx, vy);
+      const int gi = goal_index(post ? S.rpost[k] : S.rpre[k], k, N, NL);
+      r[0] = S.ps[k]; r[1] = S.ps[N + k]; r[2] = vx; r[3] = vy;
+      r[4] = S.lm[gi]; r[5] = S.lm[NL + gi];
+      r[6] = S.lmsc[gi]; r[7] = S.lmsc[NL + gi]; r[8] = S.lm[3 * NL + gi]; r[9] = 0.0;
+    } else {
+      const int l = k - N;
+      r[0] = S.lm[l]; r[1] = S.lm[NL + l]; r[2] = 0.0; r[3] = 0.0;
+      r[4] = S.lm[l]; r[5] = S.lm[NL + l];
+      r[6] = S.lmsc[l]; r[7] = S.lmsc[NL + l]; r[8] = S.lm[3 * NL + l]; r[9] = 1.0;
+    }
+  }
+  if (lane < N) {
+    const int e = lane;
+    double vx, vy;
+    agent_vel<0>(S, N, e, true, vx, vy);
+    double* o = S.egooff + e * F;
+    o[0] = S.ps[e]; o[1] = S.ps[N + e]; o[2] = vx; o[3] = vy; o[4] = S.ps[e]; o[5] = S.ps[N + e];
+    o[6] = 0.0; o[7] = 0.0; o[8] = 0.0; o[9] = 0.0;
+  }
 }
 
 template <int DYN>
-__device__ void emit_graph(const KParams& P, Lds& S, int env) {
+__device__ __forceinline__ void emit_graph(const KParams& P, Lds& S, int env) {
   const int lane = threadIdx.x;
   const int N = P.N, E = P.E, F = P.F;
-  // node features: pairs p = e * E + k, batches of 64 staged through LDS, then copied
-  const int npairs = N * E;
-  float* node_out = P.o.node + (size_t)env * npairs * F;
-  for (int b0 = 0; b0 < npairs; b0 += WAVE) {
-    const int p = b0 + lane;
-    if (p < npairs) {
-      float f[11];
-      node_features<DYN>(P, S, p / E, p % E, f);
-      for (int q = 0; q < F; ++q) S.stage[lane * F + q] = f[q];
-    }
-    __syncthreads();
-    const int cnt = min(WAVE, npairs - b0) * F;
-    for (int q = lane; q < cnt; q += WAVE) node_out[(size_t)b0 * F + q] = S.stage[q];
-    __syncthreads();
-  }
-  // adjacency: ego e, element u = r * E + c
-  const int EE = E * E;
-  float* adj_out = P.o.adj + (size_t)env * N * EE;
-  for (int e = 0; e < N; ++e) {
-    for (int u = lane; u < EE; u += WAVE) {
-      const int r = u / E, c = u - r * E;
-      float val = 0.0f;
-      if (!masked(S, N, e, r) && !masked(S, N, e, c)) {
-        const double d = S.dist[u];
-        if (d < P.coord_range && d > 0) val = (float)d;
+  if (lane < N) S.emask[lane] = ego_mask(S, N, P.L, lane);
+  if (DYN == 0) build_rows_di(P, S);
+  __syncthreads();
+  // ---- node features --------------------------------------------------------------
+  const int EF = E * F, ntot = N * EF;
+  float* node_out = P.o.node + (size_t)env * ntot;
+  if (DYN == 0) {
+    const bool vec = (ntot & 3) == 0;
+    const int step = vec ? 4 : 1;
+    for (int q0 = lane * step; q0 < ntot; q0 += WAVE * step) {
+      int e = fdiv(q0, P.m_EF);
+      const int rem = q0 - e * EF;
+      int k = fdiv(rem, P.m_F);
+      int f = rem - k * F;
+      float v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (j < step) {
+          const int ver = (k < N && k > e) ? 0 : 1;
+          v[j] = (float)(S.feat[(ver * E + k) * F + f] - S.egooff[e * F + f]);
+          if (++f == F) { f = 0; if (++k == E) { k = 0; ++e; } }
+        }
       }
-      adj_out[(size_t)e * EE + u] = val;
+      if (vec) *(float4*)(node_out + q0) = make_float4(v[0], v[1], v[2], v[3]);
+      else node_out[q0] = v[0];
     }
+  } else {
+    const int npairs = N * E;
+    for (int b0 = 0; b0 < npairs; b0 += WAVE) {
+      const int p = b0 + lane;
+      if (p < npairs) {
+        float f[11];
+        const int e = fdiv(p, P.m_E);
+        node_features<DYN>(P, S, e, p - e * E, f);
+        for (int q = 0; q < F; ++q) S.stage[lane * F + q] = f[q];
+      }
+      __syncthreads();
+      const int cnt = min(WAVE, npairs - b0) * F;
+      for (int q = lane; q < cnt; q += WAVE) node_out[(size_t)b0 * F + q] = S.stage[q];
+      __syncthreads();
+    }
+  }
+  // ---- adjacency: ego e, row r, col c ------------------------------------------------------
+  const int EE = E * E, atot = N * EE;
+  float* adj_out = P.o.adj + (size_t)env * atot;
+  const bool vec = (atot & 3) == 0;
+  const int step = vec ? 4 : 1;
+  for (int q0 = lane * step; q0 < atot; q0 += WAVE * step) {
+    int e = fdiv(q0, P.m_EE);
+    const int u = q0 - e * EE;
+    int r = fdiv(u, P.m_E);
+    int c = u - r * E;
+    uint64_t m = S.emask[e];
+    float v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (j < step) {
+        const bool dis = (((m >> r) | (m >> c)) & 1ull) != 0;
+        const double d = S.dist[r * E + c];
+        v[j] = (!dis && d < P.coord_range && d > 0) ? (float)d : 0.0f;
+        if (++c == E) {
+          c = 0;
+          if (++r == E) { r = 0; ++e; if (e < N) m = S.emask[e]; }
+        }
+      }
+    }
+    if (vec) *(float4*)(adj_out + q0) = make_float4(v[0], v[1], v[2], v[3]);
+    else adj_out[q0] = v[0];
   }
 }
 
-__device__ inline void compute_dist(const KParams& P, Lds& S) {
+__device__ __forceinline__ void compute_dist(const KParams& P, Lds& S) {
   const int lane = threadIdx.x;
   const int N = P.N, E = P.E, NL = P.NL;
   for (int u = lane; u < E * E; u += WAVE) {
-    const int a = u / E, b = u - a * E;
+    const int a = fdiv(u, P.m_E), b = u - a * E;
     double d = 0.0;
     if (a != b) {
       const int lo = a < b ? a : b, hi = a < b ? b : a;
@@ -754,7 +849,7 @@ __device__ inline void compute_dist(const KParams& P, Lds& S) {
 }
 
 template <int DYN>
-__device__ inline void write_obs(const KParams& P, const Lds& S, int env, int i) {
+__device__ __forceinline__ void write_obs(const KParams& P, const Lds& S, int env, int i) {
   const int N = P.N, NL = P.NL;
   const int gi = goal_index(S.rpre[i], i, N, NL);
   const double gx = S.lm[gi], gy = S.lm[NL + gi], gh = S.lm[2 * NL + gi], gs = S.lm[3 * NL + gi];
@@ -782,7 +877,7 @@ __device__ inline void write_obs(const KParams& P, const Lds& S, int env, int i)
   }
 }
 
-__device__ inline void summary(const KParams& P, const double* st, int N, const int32_t* reached,
+__device__ __forceinline__ void summary(const KParams& P, const double* st, int N, const int32_t* reached,
                                double* scratch, double* out) {
   // save_summary_of_episode (environment.py:895-911); st = stats [NSTAT][N]
   const double* tl = st;
@@ -813,7 +908,7 @@ __device__ inline void summary(const KParams& P, const double* st, int N, const 
 
 // Device reset of one env (MultiAgentGraphEnv.reset, environment.py:1046-1074).
 template <int DYN>
-__device__ void reset_env(const KParams& P, Lds& S, int env) {
+__device__ __forceinline__ void reset_env(const KParams& P, Lds& S, int env) {
   const int lane = threadIdx.x;
   const int N = P.N, NL = P.NL;
   double* stats = P.s.stats + (size_t)env * NSTAT * N;
@@ -841,7 +936,7 @@ __device__ void reset_env(const KParams& P, Lds& S, int env) {
   sp.goal_speed_min = P.gs_min; sp.goal_speed_max = P.gs_max;
   sp.ratio_airtaxi = S.cur[C_RAT]; sp.ratio_scenario = S.cur[C_RSC]; sp.two_pi = P.two_pi; sp.pi = P.pi;
   // every lane runs the identical draw sequence and stores the identical values
-  random_scenario(rng, sp, S.ps, S.lm);
+  random_scenario(rng, sp, S.ps, S.lm, S.scen);
   __syncthreads();
   if (lane == 0) S.mt[MT_N] = (uint32_t)rng.pos;
   __syncthreads();
@@ -876,7 +971,7 @@ __device__ void reset_env(const KParams& P, Lds& S, int env) {
 }
 
 template <int DYN>
-__device__ void store_state(const KParams& P, const Lds& S, int env) {
+__device__ __forceinline__ void store_state(const KParams& P, const Lds& S, int env) {
   const int lane = threadIdx.x;
   const int N = P.N, NL = P.NL;
   for (int k = lane; k < 4 * N; k += WAVE) {
@@ -930,10 +1025,11 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams P) {
   if (P.emit_edges) {
     compute_dist(P, S);
     uint8_t* eo = P.o.edges + (size_t)env * E * E;
+    const uint64_t m0 = ego_mask(S, N, P.L, N);
     for (int u = lane; u < E * E; u += WAVE) {
-      const int r = u / E, c = u - r * E;
+      const int r = fdiv(u, P.m_E), c = u - r * E;
       double d = S.dist[u];
-      if (masked(S, N, N, r) || masked(S, N, N, c)) d = 0.0;
+      if (((m0 >> r) | (m0 >> c)) & 1ull) d = 0.0;
       eo[u] = (d <= P.coord_range && d > 0) ? 1 : 0;
     }
   }
@@ -1146,15 +1242,15 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams P) {
   __syncthreads();
   if (lane < N) {
     const int i = lane;
-    double* sc = S.scratch;  // per-lane private copies below
-    double dsnap[MAXN], tsnap[MAXN], tmp[MAXN];
-    for (int j = 0; j < N; ++j) {
-      dsnap[j] = (j <= i) ? S.wnew[j] : S.wold[j];
-      tsnap[j] = (j <= i) ? S.wnew[N + j] : S.wold[N + j];
-    }
-    (void)sc;
-    const double dm = np_mean(dsnap, N), ds = np_std(dsnap, N, tmp);
-    const double tm = np_mean(tsnap, N), ts = np_std(tsnap, N, tmp);
+    struct Snap {
+      const double* nw;
+      const double* od;
+      int i;
+      __device__ double operator()(int j) const { return j <= i ? nw[j] : od[j]; }
+    };
+    double dm, ds, tm, ts;
+    np_mean_std(Snap{S.wnew, S.wold, i}, N, dm, ds);
+    np_mean_std(Snap{S.wnew + N, S.wold + N, i}, N, tm, ts);
     double* inf = P.o.info + ((size_t)env * N + i) * LSM_INFO_FIELDS;
     const double* winfo = P.s.winfo + (size_t)env * NWINFO * N;
     const double mr = P.s.minrel[(size_t)env * N + i];
@@ -1188,8 +1284,9 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams P) {
       stats[N + i] += blas_norm2(vx, vy) * P.dt;
       int cnt = 0, neng = 0;
       double mn = INFINITY;
+      const uint64_t m = ego_mask(S, N, P.L, i);
       for (int j = 0; j < N; ++j) {
-        if (masked(S, N, i, i) || masked(S, N, i, j)) continue;
+        if (((m >> i) | (m >> j)) & 1ull) continue;
         const double d = S.dist[i * E + j];
         if (!(d < P.coord_range && d > 0)) continue;
         cnt++;
@@ -1320,6 +1417,11 @@ static void fill_params(const lsm_env* e, KParams& P) {
   P.at_amax = 0.002; P.at_amin = -0.001; P.at_wmax = 0.1;
   P.at_thr_amax = P.at_vmax - 1.0 * 0.002; P.at_thr_amin = P.at_vmin - 1.0 * -0.001;
   P.at_box_w = (float)0.1; P.at_box_amax = (float)0.002; P.at_box_amin = (float)-0.001;
+  auto magic = [](uint32_t d) { return (uint32_t)((((uint64_t)1 << 32) + d - 1) / d); };
+  P.m_E = magic(e->E);
+  P.m_EE = magic(e->E * e->E);
+  P.m_EF = magic(e->E * e->F);
+  P.m_F = magic(e->F);
   P.ttr_max = e->ttr_max;
   P.val = e->val;
   P.ttr = e->ttr;
@@ -1575,8 +1677,8 @@ int lsm_host_scenario(const lsm_config* cfg, const lsm_curriculum* cur, uint32_t
   sp.goal_speed_max = di ? 0.5 : 110 * 0.514444 * 0.001;
   sp.ratio_airtaxi = cur->ratio_airtaxi; sp.ratio_scenario = cur->ratio_scenario;
   sp.pi = 3.141592653589793; sp.two_pi = 2 * sp.pi;
-  std::vector<double> st(4 * N), lm(4 * NL);
-  random_scenario(m, sp, st.data(), lm.data());
+  std::vector<double> st(4 * N), lm(4 * NL), ws(SCEN_WS);
+  random_scenario(m, sp, st.data(), lm.data(), ws.data());
   for (int i = 0; i < N; ++i)
     for (int c = 0; c < 4; ++c) agent_state[i * 4 + c] = st[c * N + i];
   for (int k = 0; k < NL; ++k)
