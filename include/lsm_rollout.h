@@ -52,7 +52,8 @@ enum {
   LSM_OUT_INFO = 7,       /* float64 [n][N][LSM_INFO_FIELDS] info_callback numbers   */
   LSM_OUT_EDGES = 8,      /* uint8   [n][E][E] update_graph() connectivity (optional)*/
   LSM_OUT_STATE = 9,      /* float64 [n][N][4] agent state after the last call      */
-  LSM_NUM_OUT = 10
+  LSM_OUT_DEBUG_STAMPS = 10, /* uint64 [n][16] per-phase clock stamps (diagnostic build only) */
+  LSM_NUM_OUT = 11
 };
 
 /* Per-agent info fields (navigation_graph_safe.py:386-450 + environment.py:1025). */

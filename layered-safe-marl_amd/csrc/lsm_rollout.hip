@@ -35,6 +35,19 @@
 #include "lsm_numeric.h"
 #include "lsm_scenario.h"
 
+#ifdef LSM_STAMPS
+// diagnostic build only: per-phase s_memtime stamps of each env's wave (never in the product .so)
+#define STAMP(k)                                                                             \
+  do {                                                                                       \
+    __syncthreads();                                                                         \
+    if (threadIdx.x == 0 && P.stamps) P.stamps[(size_t)blockIdx.x * 16 + (k)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define STAMP(k) \
+  do {           \
+  } while (0)
+#endif
+
 namespace lsm {
 
 constexpr int WAVE = 64;
@@ -102,6 +115,7 @@ struct KParams {
   double ttr_max;
   double cur_new[NCUR];
   uint32_t m_E, m_EE, m_EF, m_F;  // ceil(2^32 / d) for exact small-numerator division
+  unsigned long long* stamps;     // LSM_OUT_DEBUG_STAMPS (diagnostic builds only)
   TableDev val, ttr;
   StateDev s;
   OutDev o;
@@ -109,32 +123,51 @@ struct KParams {
 };
 
 // ----------------------------------------------------------------------------------
-// LDS layout (dynamic, 16-byte aligned carve)
+// LDS layout (dynamic, 16-byte aligned carve). Two unions keep one env under ~9 KB at
+// N = 8 so LDS does not cap residency below the VGPR limit (16 waves / CU):
+//   U1 = {fval, aa} (step)              | {mt, scen, scratch} (reset only)
+//   U2 = {dpair, vpair, inr} (filter)   | {feat, egooff} (DI outputs) | {stage} (airtaxi outputs)
 // ----------------------------------------------------------------------------------
 struct Lds {
   double* ps;        // [4][N] agent state (after integration; velocities pre-freeze)
   double* lm;        // [4][NL]
   double* lmsc;      // [2][NL] sin/cos of landmark headings
-  double* dist;      // [E][E]
   double* raw;       // [2][N]
   double* safe;      // [2][N]
-  double* dpair;     // [N][N]
-  float* vpair;      // [N][N]
-  uint8_t* inr;      // [N][N]
   int32_t* dpre;     // [N] done before reward update
   int32_t* dpost;    // [N] done after
   int32_t* rpre;     // [N] reached_goal before
   int32_t* rpost;    // [N] reached_goal after
+  double* pdist;     // [N] travel distance (state.p_dist)
+  double* gmt;       // [N] goal_min_time
+  double* stats;     // [NSTAT][N]
+  double* winfo;     // [NWINFO][N]
+  int32_t* sfilt;    // [N]
+  int32_t* decon;    // [N]
+  double* minrel;    // [N]
+  double* adiff;     // [N]
   double* wold;      // [2][N] dists_to_goal / times_required before this step's info
   double* wnew;      // [2][N] after
-  double* scratch;   // [2][MAXN] for np.std
-  float* stage;      // [64][F]
-  uint32_t* mt;      // [MT_WORDS]
   double* cur;       // [NCUR]
   uint64_t* emask;   // [N] bit r: entity r disconnected for ego e (snapshot rule)
-  double* feat;      // [2][E][F] DI entity rows (version 0 = pre, 1 = post reward update)
-  double* egooff;    // [N][F]   DI ego offsets subtracted from the entity rows
-  double* scen;      // [SCEN_WS] scenario workspace
+  // U1
+  float* fval;       // [E][E] d if 0 < d < range else 0 (float32, unmasked)
+  double* aa;        // [N][N] float64 agent-agent distances (episode stats)
+  uint32_t* mt;      // [MT_WORDS]
+  double* scen;      // [SCEN_WS]
+  double* scratch;   // [2][MAXN]
+  // U2
+  double* dpair;     // [N][N]
+  float* vpair;      // [N][N]
+  uint8_t* inr;      // [N][N]
+  double* feat;      // [2N + NL][F] DI entity rows: agents pre, agents post, landmarks
+  double* egooff;    // [N][F] DI ego offsets
+  float* stage;      // [64][F] airtaxi node staging
+};
+
+struct LdsPlan {
+  size_t bytes;
+  size_t off[40];
 };
 
 // q / d for q * d < 2^32 (all index math here): __umulhi(q, ceil(2^32 / d))
@@ -142,56 +175,73 @@ __device__ __forceinline__ int fdiv(int q, uint32_t m) { return (int)__umulhi((u
 
 __host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
 
-__host__ __device__ inline size_t lds_bytes(int N, int NL, int E, int F) {
-  size_t b = 0;
-  b += align16(sizeof(double) * 4 * N);
-  b += align16(sizeof(double) * 4 * NL);
-  b += align16(sizeof(double) * 2 * NL);
-  b += align16(sizeof(double) * E * E);
-  b += align16(sizeof(double) * 2 * N) * 2;
-  b += align16(sizeof(double) * N * N);
-  b += align16(sizeof(float) * N * N);
-  b += align16(N * N);
-  b += align16(sizeof(int32_t) * N) * 4;
-  b += align16(sizeof(double) * 2 * N) * 2;
-  b += align16(sizeof(double) * 2 * MAXN);
-  b += align16(sizeof(float) * 64 * F);
-  b += align16(sizeof(uint32_t) * MT_WORDS);
-  b += align16(sizeof(double) * NCUR);
-  b += align16(sizeof(uint64_t) * N);
-  b += align16(sizeof(double) * 2 * E * F);
-  b += align16(sizeof(double) * N * F);
-  b += align16(sizeof(double) * SCEN_WS);
-  return b;
+// Offsets of every LDS array (shared by the host launch and the device carve).
+__host__ __device__ inline LdsPlan lds_plan(int N, int NL, int E, int F) {
+  LdsPlan p;
+  size_t o = 0;
+  int k = 0;
+  auto put = [&](size_t bytes) { p.off[k++] = o; o += align16(bytes); };
+  put(8 * 4 * N); put(8 * 4 * NL); put(8 * 2 * NL); put(8 * 2 * N); put(8 * 2 * N);
+  put(4 * N); put(4 * N); put(4 * N); put(4 * N);
+  put(8 * N); put(8 * N); put(8 * NSTAT * N); put(8 * NWINFO * N); put(4 * N); put(4 * N);
+  put(8 * N); put(8 * N); put(8 * 2 * N); put(8 * 2 * N); put(8 * NCUR); put(8 * N);
+  // U1
+  const size_t u1 = o;
+  size_t a = align16(4 * E * E), b = a + align16(8 * N * N);
+  size_t c = align16(4 * MT_WORDS), d = c + align16(8 * SCEN_WS), e = d + align16(8 * 2 * MAXN);
+  p.off[k++] = u1; p.off[k++] = u1 + a; p.off[k++] = u1; p.off[k++] = u1 + c; p.off[k++] = u1 + d;
+  o = u1 + (b > e ? b : e);
+  // U2
+  const size_t u2 = o;
+  size_t f1 = align16(8 * N * N), f2 = f1 + align16(4 * N * N), f3 = f2 + align16(N * N);
+  size_t g1 = align16(8 * (2 * N + NL) * F), g2 = g1 + align16(8 * N * F);
+  size_t h1 = align16(4 * 64 * F);
+  p.off[k++] = u2; p.off[k++] = u2 + f1; p.off[k++] = u2 + f2;
+  p.off[k++] = u2; p.off[k++] = u2 + g1; p.off[k++] = u2;
+  size_t m = f3 > g2 ? f3 : g2;
+  m = m > h1 ? m : h1;
+  m = m > (size_t)(8 * 2 * 64) ? m : (size_t)(8 * 2 * 64);   // magnetic partial sums (filter off)
+  o = u2 + m;
+  p.bytes = o;
+  return p;
 }
 
 __device__ __forceinline__ Lds carve(unsigned char* base, int N, int NL, int E, int F) {
+  const LdsPlan p = lds_plan(N, NL, E, F);
   Lds L;
-  size_t o = 0;
-  auto take = [&](size_t bytes) { unsigned char* p = base + o; o += align16(bytes); return p; };
-  L.ps = (double*)take(sizeof(double) * 4 * N);
-  L.lm = (double*)take(sizeof(double) * 4 * NL);
-  L.lmsc = (double*)take(sizeof(double) * 2 * NL);
-  L.dist = (double*)take(sizeof(double) * E * E);
-  L.raw = (double*)take(sizeof(double) * 2 * N);
-  L.safe = (double*)take(sizeof(double) * 2 * N);
-  L.dpair = (double*)take(sizeof(double) * N * N);
-  L.vpair = (float*)take(sizeof(float) * N * N);
-  L.inr = (uint8_t*)take(N * N);
-  L.dpre = (int32_t*)take(sizeof(int32_t) * N);
-  L.dpost = (int32_t*)take(sizeof(int32_t) * N);
-  L.rpre = (int32_t*)take(sizeof(int32_t) * N);
-  L.rpost = (int32_t*)take(sizeof(int32_t) * N);
-  L.wold = (double*)take(sizeof(double) * 2 * N);
-  L.wnew = (double*)take(sizeof(double) * 2 * N);
-  L.scratch = (double*)take(sizeof(double) * 2 * MAXN);
-  L.stage = (float*)take(sizeof(float) * 64 * F);
-  L.mt = (uint32_t*)take(sizeof(uint32_t) * MT_WORDS);
-  L.cur = (double*)take(sizeof(double) * NCUR);
-  L.emask = (uint64_t*)take(sizeof(uint64_t) * N);
-  L.feat = (double*)take(sizeof(double) * 2 * E * F);
-  L.egooff = (double*)take(sizeof(double) * N * F);
-  L.scen = (double*)take(sizeof(double) * SCEN_WS);
+  int k = 0;
+  L.ps = (double*)(base + p.off[k++]);
+  L.lm = (double*)(base + p.off[k++]);
+  L.lmsc = (double*)(base + p.off[k++]);
+  L.raw = (double*)(base + p.off[k++]);
+  L.safe = (double*)(base + p.off[k++]);
+  L.dpre = (int32_t*)(base + p.off[k++]);
+  L.dpost = (int32_t*)(base + p.off[k++]);
+  L.rpre = (int32_t*)(base + p.off[k++]);
+  L.rpost = (int32_t*)(base + p.off[k++]);
+  L.pdist = (double*)(base + p.off[k++]);
+  L.gmt = (double*)(base + p.off[k++]);
+  L.stats = (double*)(base + p.off[k++]);
+  L.winfo = (double*)(base + p.off[k++]);
+  L.sfilt = (int32_t*)(base + p.off[k++]);
+  L.decon = (int32_t*)(base + p.off[k++]);
+  L.minrel = (double*)(base + p.off[k++]);
+  L.adiff = (double*)(base + p.off[k++]);
+  L.wold = (double*)(base + p.off[k++]);
+  L.wnew = (double*)(base + p.off[k++]);
+  L.cur = (double*)(base + p.off[k++]);
+  L.emask = (uint64_t*)(base + p.off[k++]);
+  L.fval = (float*)(base + p.off[k++]);
+  L.aa = (double*)(base + p.off[k++]);
+  L.mt = (uint32_t*)(base + p.off[k++]);
+  L.scen = (double*)(base + p.off[k++]);
+  L.scratch = (double*)(base + p.off[k++]);
+  L.dpair = (double*)(base + p.off[k++]);
+  L.vpair = (float*)(base + p.off[k++]);
+  L.inr = (uint8_t*)(base + p.off[k++]);
+  L.feat = (double*)(base + p.off[k++]);
+  L.egooff = (double*)(base + p.off[k++]);
+  L.stage = (float*)(base + p.off[k++]);
   return L;
 }
 
@@ -410,42 +460,82 @@ __device__ __forceinline__ bool goal_reached(const KParams& P, const Lds& S, int
   return dist < mdt && cond && verr < gse;
 }
 
-// double_integrator_velocity_error_from_magnetic_field_reference (utils.py:276-349)
-__device__ __forceinline__ double magnetic_penalty(const KParams& P, double px, double py, double vx, double vy,
-                                          double gx, double gy, double gh, double gs, double radius) {
+// double_integrator_velocity_error_from_magnetic_field_reference (utils.py:276-349).
+// The 50-segment Biot-Savart sum is split over G lanes per agent (segments g, g+G, ...);
+// the G partial sums are combined in lane order (float64; ulp-level vs the reference's
+// sequential sum, reward tolerance). Called by ALL lanes; returns the penalty in lanes
+// lane < N (agent = lane), garbage elsewhere.
+__device__ __forceinline__ double magnetic_penalty_wave(const KParams& P, Lds& S, double* part) {
+  const int lane = threadIdx.x;
+  const int N = P.N, NL = P.NL;
+  int G = 1;
+  while (G * 2 * N <= WAVE) G *= 2;
+  const int a = lane / G, g = lane - a * G;
+  const bool act = a < N;
+  const int ai = act ? a : 0;
+  const int gi = goal_index(S.rpre[ai], ai, N, NL);
+  const double gx = S.lm[gi], gy = S.lm[NL + gi], gh = S.lm[2 * NL + gi];
+  const double px = S.ps[ai], py = S.ps[N + ai];
   const double ch = cos(gh), sh = sin(gh);
-  double rpx, rpy, rvx, rvy;
+  double rpx, rpy;
   blas_rot(ch, sh, px - gx, py - gy, rpx, rpy);
-  const double dist = blas_norm2(rpx, rpy);
-  const double polar = atan2(rpy, rpx);
-  blas_rot(ch, sh, vx - 0.0, vy - 0.0, rvx, rvy);
-  double href = 0.0;
-  if (!(fabs(rpx) < 1e-6)) {
+  const double radius = 2 * S.cur[C_MDT];
+  double m0 = 0.0, m1 = 0.0;
+  if (act && !(fabs(rpx) < 1e-6)) {
     const double x = 0.5 * rpx, y = rpy;
-    double m0 = 0.0, m1 = 0.0;
     const double nr = -radius;
-    for (int k = 0; k < 50; ++k) {
+    for (int k = g; k < 50; k += G) {
       const double Ly = nr * P.mag_c[k], Lz = nr * P.mag_s[k];
       const double dLy = radius * P.mag_s[k], dLz = nr * P.mag_c[k];
       const double r0 = x - 0.0, r1 = y - Ly, r2 = 0.0 - Lz;
-      const double r3 = pow(blas_norm3(r0, r1, r2), 3.0);
+      const double rn = blas_norm3(r0, r1, r2);
+      const double sq = rn * rn;
+      const double r3 = fma(sq, rn, fma(rn, rn, -sq) * rn);   // rn**3, ~correctly rounded
       const double c0 = dLy * r2 - dLz * r1;
       const double c1 = dLz * r0 - 0.0 * r2;
       m0 += c0 / r3;
       m1 += c1 / r3;
     }
-    m0 = m0 / 0.5;
-    href = atan2(m1, m0);
   }
-  double ref_speed = py_max(gs, 0.1);
-  const double dr = np_clip(dist / 1.5, 0, 1);
-  ref_speed = ref_speed * (1 - dr) + 1.0 * dr;
-  const double rfx = ref_speed * cos(href), rfy = ref_speed * sin(href);
-  const double err = blas_norm2(rvx - rfx, rvy - rfy);
-  const double cp = cos(polar);
-  if (cp < P.cos_pi6) return err;
-  const double ar = np_clip((cp - P.cos_pi6) / (1 - P.cos_pi6), 0, 1);
-  return err * (1 - ar) + dist * ar;
+  part[lane] = m0;
+  part[WAVE + lane] = m1;
+  __syncthreads();
+  double pen = 0.0;
+  if (lane < N) {
+    const int i = lane;
+    const int gj = goal_index(S.rpre[i], i, N, NL);
+    const double gxx = S.lm[gj], gyy = S.lm[NL + gj], ghh = S.lm[2 * NL + gj], gs = S.lm[3 * NL + gj];
+    const double c = cos(ghh), s = sin(ghh);
+    double qx, qy, rvx, rvy;
+    blas_rot(c, s, S.ps[i] - gxx, S.ps[N + i] - gyy, qx, qy);
+    const double dist = blas_norm2(qx, qy);
+    const double polar = atan2(qy, qx);
+    blas_rot(c, s, S.ps[2 * N + i] - 0.0, S.ps[3 * N + i] - 0.0, rvx, rvy);
+    double href = 0.0;
+    if (!(fabs(qx) < 1e-6)) {
+      double s0 = 0.0, s1 = 0.0;
+      for (int q = 0; q < G; ++q) {
+        s0 += part[i * G + q];
+        s1 += part[WAVE + i * G + q];
+      }
+      s0 = s0 / 0.5;
+      href = atan2(s1, s0);
+    }
+    double ref_speed = py_max(gs, 0.1);
+    const double dr = np_clip(dist / 1.5, 0, 1);
+    ref_speed = ref_speed * (1 - dr) + 1.0 * dr;
+    const double rfx = ref_speed * cos(href), rfy = ref_speed * sin(href);
+    const double err = blas_norm2(rvx - rfx, rvy - rfy);
+    const double cp = cos(polar);
+    if (cp < P.cos_pi6) {
+      pen = err;
+    } else {
+      const double ar = np_clip((cp - P.cos_pi6) / (1 - P.cos_pi6), 0, 1);
+      pen = err * (1 - ar) + dist * ar;
+    }
+  }
+  __syncthreads();
+  return pen;
 }
 
 __device__ __forceinline__ double seqdot4(const double* a, const double* b) {
@@ -720,16 +810,16 @@ __device__ __forceinline__ uint64_t ego_mask(const Lds& S, int N, int L, int e) 
   return m;
 }
 
-// DI node features are (entity row) - (ego offset): build both once per step in LDS.
+// DI node features are (entity row) - (ego offset): rows for agents (pre, post update) and
+// landmarks, offsets per ego, built once per step in LDS (utils.py:201-255).
 __device__ __forceinline__ void build_rows_di(const KParams& P, Lds& S) {
   const int lane = threadIdx.x;
-  const int N = P.N, NL = P.NL, E = P.E, F = P.F;
-  for (int t = lane; t < 2 * E; t += WAVE) {
-    const int v = t >= E ? 1 : 0;
-    const int k = t - v * E;
-    double* r = S.feat + (size_t)(v * E + k) * F;
-    if (k < N) {
-      const bool post = v == 1;
+  const int N = P.N, NL = P.NL, F = P.F;
+  for (int t = lane; t < 2 * N + NL; t += WAVE) {
+    double* r = S.feat + (size_t)t * F;
+    if (t < 2 * N) {
+      const bool post = t >= N;
+      const int k = post ? t - N : t;
       double vx, vy;
       agent_vel<0>(S, N, k, post, vx, vy);
       const int gi = goal_index(post ? S.rpost[k] : S.rpre[k], k, N, NL);
@@ -737,7 +827,7 @@ __device__ __forceinline__ void build_rows_di(const KParams& P, Lds& S) {
       r[4] = S.lm[gi]; r[5] = S.lm[NL + gi];
       r[6] = S.lmsc[gi]; r[7] = S.lmsc[NL + gi]; r[8] = S.lm[3 * NL + gi]; r[9] = 0.0;
     } else {
-      const int l = k - N;
+      const int l = t - 2 * N;
       r[0] = S.lm[l]; r[1] = S.lm[NL + l]; r[2] = 0.0; r[3] = 0.0;
       r[4] = S.lm[l]; r[5] = S.lm[NL + l];
       r[6] = S.lmsc[l]; r[7] = S.lmsc[NL + l]; r[8] = S.lm[3 * NL + l]; r[9] = 1.0;
@@ -753,11 +843,12 @@ __device__ __forceinline__ void build_rows_di(const KParams& P, Lds& S) {
   }
 }
 
+// node_obs [N][E][F] and adj [N][E][E] of one env (float4 stores when the env block is
+// 16-byte aligned). S.emask must hold the per-ego masks; S.fval the thresholded distances.
 template <int DYN>
 __device__ __forceinline__ void emit_graph(const KParams& P, Lds& S, int env) {
   const int lane = threadIdx.x;
   const int N = P.N, E = P.E, F = P.F;
-  if (lane < N) S.emask[lane] = ego_mask(S, N, P.L, lane);
   if (DYN == 0) build_rows_di(P, S);
   __syncthreads();
   // ---- node features --------------------------------------------------------------
@@ -775,8 +866,8 @@ __device__ __forceinline__ void emit_graph(const KParams& P, Lds& S, int env) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         if (j < step) {
-          const int ver = (k < N && k > e) ? 0 : 1;
-          v[j] = (float)(S.feat[(ver * E + k) * F + f] - S.egooff[e * F + f]);
+          const int row = (k < N) ? ((k > e) ? k : N + k) : N + k;
+          v[j] = (float)(S.feat[row * F + f] - S.egooff[e * F + f]);
           if (++f == F) { f = 0; if (++k == E) { k = 0; ++e; } }
         }
       }
@@ -815,8 +906,7 @@ __device__ __forceinline__ void emit_graph(const KParams& P, Lds& S, int env) {
     for (int j = 0; j < 4; ++j) {
       if (j < step) {
         const bool dis = (((m >> r) | (m >> c)) & 1ull) != 0;
-        const double d = S.dist[r * E + c];
-        v[j] = (!dis && d < P.coord_range && d > 0) ? (float)d : 0.0f;
+        v[j] = dis ? 0.0f : S.fval[r * E + c];
         if (++c == E) {
           c = 0;
           if (++r == E) { r = 0; ++e; if (e < N) m = S.emask[e]; }
@@ -828,6 +918,8 @@ __device__ __forceinline__ void emit_graph(const KParams& P, Lds& S, int env) {
   }
 }
 
+// cached_dist_mag (core.py:514-543): float32 thresholded copy for the adjacency
+// (adj = d * (d < range) * (d > 0), navigation_graph_safe.py:991-992) + float64 agent block.
 __device__ __forceinline__ void compute_dist(const KParams& P, Lds& S) {
   const int lane = threadIdx.x;
   const int N = P.N, E = P.E, NL = P.NL;
@@ -843,7 +935,8 @@ __device__ __forceinline__ void compute_dist(const KParams& P, Lds& S) {
       const double dx = xa - xb, dy = ya - yb;
       d = sqrt(dx * dx + dy * dy);
     }
-    S.dist[u] = d;
+    S.fval[u] = (d < P.coord_range && d > 0) ? (float)d : 0.0f;
+    if (a < N && b < N) S.aa[a * N + b] = d;
   }
   __syncthreads();
 }
@@ -877,21 +970,21 @@ __device__ __forceinline__ void write_obs(const KParams& P, const Lds& S, int en
   }
 }
 
-__device__ __forceinline__ void summary(const KParams& P, const double* st, int N, const int32_t* reached,
-                               double* scratch, double* out) {
-  // save_summary_of_episode (environment.py:895-911); st = stats [NSTAT][N]
-  const double* tl = st;
-  const double* td = st + N;
-  const double* dn = st + 2 * N;
-  const double* cf = st + 3 * N;
-  const double* md = st + 4 * N;
-  const double* mu = st + 5 * N;
-  double* a = scratch;
-  double* b = scratch + MAXN;
+// save_summary_of_episode (environment.py:895-911) from the LDS copy of the stats.
+__device__ __forceinline__ void summary(const KParams& P, const Lds& S, double* out) {
+  const int N = P.N;
+  const double* tl = S.stats;
+  const double* td = S.stats + N;
+  const double* dn = S.stats + 2 * N;
+  const double* cf = S.stats + 3 * N;
+  const double* md = S.stats + 4 * N;
+  const double* mu = S.stats + 5 * N;
+  double* a = S.scratch;
+  double* b = S.scratch + MAXN;
   out[0] = P.dt * np_mean(tl, N);
   out[1] = np_mean(td, N);
   out[2] = np_mean(dn, N);
-  for (int i = 0; i < N; ++i) a[i] = (double)reached[i];
+  for (int i = 0; i < N; ++i) a[i] = (double)S.rpost[i];
   out[3] = np_mean(a, N);
   for (int i = 0; i < N; ++i) b[i] = (tl[i] == 0) ? 1.0 : tl[i];
   for (int i = 0; i < N; ++i) a[i] = cf[i] / b[i];
@@ -906,25 +999,26 @@ __device__ __forceinline__ void summary(const KParams& P, const double* st, int 
   if (out[6] == INFINITY) out[6] = P.coord_range;
 }
 
-// Device reset of one env (MultiAgentGraphEnv.reset, environment.py:1046-1074).
+// Device reset of one env (MultiAgentGraphEnv.reset, environment.py:1046-1074). Expects the
+// env's persistent per-agent arrays in LDS (S.stats, S.rpost = reached_goal before reset).
 template <int DYN>
 __device__ __forceinline__ void reset_env(const KParams& P, Lds& S, int env) {
   const int lane = threadIdx.x;
   const int N = P.N, NL = P.NL;
-  double* stats = P.s.stats + (size_t)env * NSTAT * N;
   double* prev = P.s.prev + (size_t)env * 8;
-  // summary of the finishing episode (uses reached_goal before the reset)
   if (lane == 0) {
     double outv[8];
-    summary(P, stats, N, S.rpost, S.scratch, outv);
-    for (int k = 0; k < 8; ++k) prev[k] = outv[k];
+    summary(P, S, outv);
+    for (int k = 0; k < 8; ++k) {
+      prev[k] = outv[k];
+      P.o.ep_info[(size_t)env * 8 + k] = outv[k];
+    }
   }
-  // curriculum for this env
+  __syncthreads();
   for (int k = lane; k < NCUR; k += WAVE) {
     S.cur[k] = P.cur_new[k];
     P.s.cur[(size_t)env * NCUR + k] = P.cur_new[k];
   }
-  // RNG state -> LDS
   const uint32_t* mtg = P.s.mt + (size_t)env * MT_WORDS;
   for (int k = lane; k < MT_WORDS; k += WAVE) S.mt[k] = mtg[k];
   __syncthreads();
@@ -948,30 +1042,22 @@ __device__ __forceinline__ void reset_env(const KParams& P, Lds& S, int env) {
   }
   for (int k = lane; k < N; k += WAVE) {
     S.dpre[k] = 0; S.dpost[k] = 0; S.rpre[k] = 0; S.rpost[k] = 0;
+    S.emask[k] = 0;
+    S.winfo[k] = -1.0; S.winfo[N + k] = -1.0; S.winfo[2 * N + k] = -1.0; S.winfo[3 * N + k] = 0.0;
+    for (int q = 0; q < NSTAT; ++q) S.stats[q * N + k] = (q == 4) ? INFINITY : 0.0;
+    S.pdist[k] = 0.0;
+    S.gmt[k] = plain_norm2(S.ps[k] - S.lm[k], S.ps[N + k] - S.lm[NL + k]) / P.max_speed;
   }
-  __syncthreads();
+  if (lane == 0) P.s.step[env] = 0;
+  __syncthreads();   // MT words read out of U1 before compute_dist overwrites it
   compute_dist(P, S);
-  // per-agent reset of world metrics / stats / goal_min_time
-  if (lane < N) {
-    const int i = lane;
-    double* winfo = P.s.winfo + (size_t)env * NWINFO * N;
-    winfo[i] = -1.0; winfo[N + i] = -1.0; winfo[2 * N + i] = -1.0; winfo[3 * N + i] = 0.0;
-    for (int k = 0; k < NSTAT; ++k) stats[k * N + i] = (k == 4) ? INFINITY : 0.0;
-    P.s.pdist[(size_t)env * N + i] = 0.0;
-    const double gmt = plain_norm2(S.ps[i] - S.lm[i], S.ps[N + i] - S.lm[NL + i]) / P.max_speed;
-    P.s.gmt[(size_t)env * N + i] = gmt;
-    write_obs<DYN>(P, S, env, i);
-  }
-  if (lane == 0) {
-    P.s.step[env] = 0;
-    for (int k = 0; k < 8; ++k) P.o.ep_info[(size_t)env * 8 + k] = prev[k];
-  }
-  __syncthreads();
+  if (lane < N) write_obs<DYN>(P, S, env, lane);
   emit_graph<DYN>(P, S, env);
 }
 
+// Persistent per-env arrays: LDS -> HBM.
 template <int DYN>
-__device__ __forceinline__ void store_state(const KParams& P, const Lds& S, int env) {
+__device__ __forceinline__ void store_state(const KParams& P, const Lds& S, int env, bool lm_changed) {
   const int lane = threadIdx.x;
   const int N = P.N, NL = P.NL;
   for (int k = lane; k < 4 * N; k += WAVE) {
@@ -981,11 +1067,21 @@ __device__ __forceinline__ void store_state(const KParams& P, const Lds& S, int 
     P.s.st[(size_t)env * 4 * N + k] = v;
     if (P.o.state) P.o.state[((size_t)env * N + j) * 4 + c] = v;
   }
-  for (int k = lane; k < 4 * NL; k += WAVE) P.s.lm[(size_t)env * 4 * NL + k] = S.lm[k];
+  if (lm_changed)
+    for (int k = lane; k < 4 * NL; k += WAVE) P.s.lm[(size_t)env * 4 * NL + k] = S.lm[k];
   for (int k = lane; k < N; k += WAVE) {
-    P.s.done[(size_t)env * N + k] = (uint8_t)S.dpost[k];
-    P.s.reached[(size_t)env * N + k] = S.rpost[k];
+    const size_t o = (size_t)env * N + k;
+    P.s.done[o] = (uint8_t)S.dpost[k];
+    P.s.reached[o] = S.rpost[k];
+    P.s.pdist[o] = S.pdist[k];
+    P.s.gmt[o] = S.gmt[k];
+    P.s.sfilt[o] = (uint8_t)S.sfilt[k];
+    P.s.decon[o] = S.decon[k];
+    P.s.minrel[o] = S.minrel[k];
+    P.s.adiff[o] = S.adiff[k];
   }
+  for (int k = lane; k < NSTAT * N; k += WAVE) P.s.stats[(size_t)env * NSTAT * N + k] = S.stats[k];
+  for (int k = lane; k < NWINFO * N; k += WAVE) P.s.winfo[(size_t)env * NWINFO * N + k] = S.winfo[k];
 }
 
 template <int DYN>
@@ -995,49 +1091,29 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams P) {
   const int lane = threadIdx.x;
   const int N = P.N, NL = P.NL, E = P.E;
   Lds S = carve(smem, N, NL, E, P.F);
+  STAMP(0);
 
-  // ---- load env state ------------------------------------------------------------
+  // ---- 0. one batch of coalesced loads of everything the env keeps in HBM ------------
   for (int k = lane; k < 4 * N; k += WAVE) S.ps[k] = P.s.st[(size_t)env * 4 * N + k];
   for (int k = lane; k < 4 * NL; k += WAVE) S.lm[k] = P.s.lm[(size_t)env * 4 * NL + k];
+  for (int k = lane; k < NSTAT * N; k += WAVE) S.stats[k] = P.s.stats[(size_t)env * NSTAT * N + k];
+  for (int k = lane; k < NWINFO * N; k += WAVE) S.winfo[k] = P.s.winfo[(size_t)env * NWINFO * N + k];
   for (int k = lane; k < N; k += WAVE) {
-    const int d = P.s.done[(size_t)env * N + k];
-    const int r = P.s.reached[(size_t)env * N + k];
+    const size_t o = (size_t)env * N + k;
+    const int d = P.s.done[o];
+    const int r = P.s.reached[o];
     S.dpre[k] = d; S.dpost[k] = d; S.rpre[k] = r; S.rpost[k] = r;
+    S.pdist[k] = P.s.pdist[o];
+    S.gmt[k] = P.s.gmt[o];
+    S.sfilt[k] = P.s.sfilt[o];
+    S.decon[k] = P.s.decon[o];
+    S.minrel[k] = P.s.minrel[o];
+    S.adiff[k] = P.s.adiff[o];
   }
   for (int k = lane; k < NCUR; k += WAVE) S.cur[k] = P.s.cur[(size_t)env * NCUR + k];
-  __syncthreads();
-
-  if (P.mode == 1) {
-    for (int k = lane; k < N; k += WAVE) S.rpost[k] = S.rpre[k];
-    __syncthreads();
-    reset_env<DYN>(P, S, env);
-    __syncthreads();
-    store_state<DYN>(P, S, env);
-    return;
-  }
-
-  for (int k = lane; k < NL; k += WAVE) {
-    S.lmsc[k] = sin(S.lm[2 * NL + k]);
-    S.lmsc[NL + k] = cos(S.lm[2 * NL + k]);
-  }
-
-  // ---- 1. update_graph() at step start (previous state, final masks) --------------
-  if (P.emit_edges) {
-    compute_dist(P, S);
-    uint8_t* eo = P.o.edges + (size_t)env * E * E;
-    const uint64_t m0 = ego_mask(S, N, P.L, N);
-    for (int u = lane; u < E * E; u += WAVE) {
-      const int r = fdiv(u, P.m_E), c = u - r * E;
-      double d = S.dist[u];
-      if (((m0 >> r) | (m0 >> c)) & 1ull) d = 0.0;
-      eo[u] = (d <= P.coord_range && d > 0) ? 1 : 0;
-    }
-  }
-
-  // ---- 2. decode actions ----------------------------------------------------------
-  if (lane < N) {
+  int ai = 0;
+  if (P.mode == 0 && lane < N) {
     const size_t base = (size_t)env * N + lane;
-    int ai = 0;
     if (P.action_kind == LSM_ACTIONS_INDEX_I32) {
       ai = ((const int32_t*)P.actions)[base];
     } else if (P.action_kind == LSM_ACTIONS_ONEHOT_F32) {
@@ -1049,12 +1125,53 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams P) {
       double best = a[0];
       for (int q = 1; q < 25; ++q) if (a[q] > best) { best = a[q]; ai = q; }
     }
-    ai = ai < 0 ? 0 : (ai > 24 ? 24 : ai);
-    const int xi = ai / 5, yi = ai - xi * 5;
+  }
+  const int cstep = P.s.step[env] + 1;
+  __syncthreads();
+  STAMP(1);
+
+  if (P.mode == 1) {
+    reset_env<DYN>(P, S, env);
+    __syncthreads();
+    store_state<DYN>(P, S, env, true);
+    return;
+  }
+
+  for (int k = lane; k < NL; k += WAVE) {
+    S.lmsc[k] = sin(S.lm[2 * NL + k]);
+    S.lmsc[NL + k] = cos(S.lm[2 * NL + k]);
+  }
+
+  // ---- 1. update_graph() at step start (previous state, final masks) --------------
+  if (P.emit_edges) {
+    uint8_t* eo = P.o.edges + (size_t)env * E * E;
+    const uint64_t m0 = ego_mask(S, N, P.L, N);
+    for (int u = lane; u < E * E; u += WAVE) {
+      const int a = fdiv(u, P.m_E), b = u - a * E;
+      double d = 0.0;
+      if (a != b) {
+        const int lo = a < b ? a : b, hi = a < b ? b : a;
+        const double xa = lo < N ? S.ps[lo] : S.lm[lo - N];
+        const double ya = lo < N ? S.ps[N + lo] : S.lm[NL + lo - N];
+        const double xb = hi < N ? S.ps[hi] : S.lm[hi - N];
+        const double yb = hi < N ? S.ps[N + hi] : S.lm[NL + hi - N];
+        const double dx = xa - xb, dy = ya - yb;
+        d = sqrt(dx * dx + dy * dy);
+      }
+      if (((m0 >> a) | (m0 >> b)) & 1ull) d = 0.0;
+      eo[u] = (d <= P.coord_range && d > 0) ? 1 : 0;
+    }
+  }
+
+  // ---- 2. decode actions ----------------------------------------------------------
+  if (lane < N) {
+    int a = ai < 0 ? 0 : (ai > 24 ? 24 : ai);
+    const int xi = a / 5, yi = a - xi * 5;
     S.raw[lane] = P.act0[xi];
     S.raw[N + lane] = P.act1[yi];
   }
   __syncthreads();
+  STAMP(2);
 
   // ---- 3. safety filter ---------------------------------------------------------------
   const bool filter_on = S.cur[C_FILT] != 0.0;
@@ -1075,6 +1192,7 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams P) {
     }
     __syncthreads();
   }
+  STAMP(3);
   if (lane < N) {
     const int i = lane;
     double u0 = S.raw[i], u1 = S.raw[N + i];
@@ -1082,14 +1200,15 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams P) {
       uint8_t fl = 0;
       int dec = -1;
       if (!S.dpre[i]) filter_ego<DYN>(P, S, i, fl, dec, u0, u1);
-      P.s.sfilt[(size_t)env * N + i] = fl;
-      P.s.decon[(size_t)env * N + i] = dec;
+      S.sfilt[i] = fl;
+      S.decon[i] = dec;
     }
     S.safe[i] = u0;
     S.safe[N + i] = u1;
-    P.s.adiff[(size_t)env * N + i] = blas_norm2(S.raw[i] - u0, S.raw[N + i] - u1);
+    S.adiff[i] = blas_norm2(S.raw[i] - u0, S.raw[N + i] - u1);
   }
   __syncthreads();
+  STAMP(4);
 
   // ---- 4. integrate ----------------------------------------------------------------------
   if (lane < N && !S.dpre[lane]) {
@@ -1129,9 +1248,10 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams P) {
       spd = s3;
     }
     S.ps[i] = x; S.ps[N + i] = y; S.ps[2 * N + i] = s2; S.ps[3 * N + i] = s3;
-    P.s.pdist[(size_t)env * N + i] += spd * dt;
+    S.pdist[i] += spd * dt;
   }
   __syncthreads();
+  STAMP(5);
 
   // ---- 5. distances, min relative distance ---------------------------------------------
   compute_dist(P, S);
@@ -1145,20 +1265,24 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams P) {
         m = (d < m) ? d : m;
       }
     }
-    P.s.minrel[(size_t)env * N + i] = m;
+    S.minrel[i] = m;
   }
-  const int cstep = P.s.step[env] + 1;
+  STAMP(6);
 
   // ---- 6. obs, reward, goal/done update ---------------------------------------------------
+  double mag = 0.0;
+  if (DYN == 0 && !P.use_filter_arg) mag = magnetic_penalty_wave(P, S, S.dpair);
   double rew = 0.0;
+  double th_pre = 0.0, spd_pre = 0.0;
   if (lane < N) {
     const int i = lane;
     write_obs<DYN>(P, S, env, i);
     const int gi = goal_index(S.rpre[i], i, N, NL);
     const double gx = S.lm[gi], gy = S.lm[NL + gi], gh = S.lm[2 * NL + gi], gs = S.lm[3 * NL + gi];
     const double px = S.ps[i], py = S.ps[N + i];
-    const double th = agent_theta<DYN>(S, N, i, false);
-    const double spd = agent_speed<DYN>(S, N, i, false);
+    th_pre = agent_theta<DYN>(S, N, i, false);
+    spd_pre = agent_speed<DYN>(S, N, i, false);
+    const double th = th_pre, spd = spd_pre;
     const double he = dae(th, gh);
     const double hpr = 1 - np_clip(he / S.cur[C_GHE], 0, 1);
     const double se = fabs(spd - gs);
@@ -1180,9 +1304,7 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams P) {
     if (!done0) {
       if (DYN == 0) {
         if (!P.use_filter_arg) {
-          double vx, vy;
-          agent_vel<DYN>(S, N, i, false, vx, vy);
-          double pen = 3 * magnetic_penalty(P, px, py, vx, vy, gx, gy, gh, gs, 2 * S.cur[C_MDT]);
+          double pen = 3 * mag;
           pen = np_clip(1 - S.cur[C_SLOPED], 0, 1) * pen;
           r = r - pen;
         }
@@ -1211,17 +1333,18 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams P) {
     P.o.rew[(size_t)env * N + i] = (float)rew;
   }
   __syncthreads();
+  if (lane < N) S.emask[lane] = ego_mask(S, N, P.L, lane);
+  STAMP(7);
 
   // ---- 7/8. info_callback numbers -----------------------------------------------------
   if (lane < N) {
     const int i = lane;
-    double* winfo = P.s.winfo + (size_t)env * NWINFO * N;
-    const double tr_old = winfo[i], dg_old = winfo[N + i];
+    const double tr_old = S.winfo[i], dg_old = S.winfo[N + i];
     S.wold[i] = dg_old; S.wold[N + i] = tr_old;
-    double tr = tr_old, dg = dg_old, dl = winfo[2 * N + i];
+    double tr = tr_old, dg = dg_old, dl = S.winfo[2 * N + i];
     const int gi = goal_index(S.rpost[i], i, N, NL);
     const double dist = plain_norm2(S.ps[i] - S.lm[gi], S.ps[N + i] - S.lm[NL + gi]);
-    const double pd = P.s.pdist[(size_t)env * N + i];
+    const double pd = S.pdist[i];
     if (goal_reached<DYN>(P, S, i, true, S.rpost[i]) && tr == -1) {
       tr = cstep * P.dt;
       dg = pd;
@@ -1231,12 +1354,12 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams P) {
       dg = pd;
       dl = dist;
     }
-    double nc = winfo[3 * N + i];
+    double nc = S.winfo[3 * N + i];
     for (int a = 0; a < N; ++a) {
       if (a == i) continue;
       if (blas_norm2(S.ps[i] - S.ps[a], S.ps[N + i] - S.ps[N + a]) < 1.05 * (0.05 + 0.05)) nc += 1;
     }
-    winfo[i] = tr; winfo[N + i] = dg; winfo[2 * N + i] = dl; winfo[3 * N + i] = nc;
+    S.winfo[i] = tr; S.winfo[N + i] = dg; S.winfo[2 * N + i] = dl; S.winfo[3 * N + i] = nc;
     S.wnew[i] = dg; S.wnew[N + i] = tr;
   }
   __syncthreads();
@@ -1252,73 +1375,76 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams P) {
     np_mean_std(Snap{S.wnew, S.wold, i}, N, dm, ds);
     np_mean_std(Snap{S.wnew + N, S.wold + N, i}, N, tm, ts);
     double* inf = P.o.info + ((size_t)env * N + i) * LSM_INFO_FIELDS;
-    const double* winfo = P.s.winfo + (size_t)env * NWINFO * N;
-    const double mr = P.s.minrel[(size_t)env * N + i];
+    const double mr = S.minrel[i];
     inf[LSM_INFO_INDIVIDUAL_REWARD] = rew;
     inf[LSM_INFO_MIN_RELATIVE_DISTANCE] = mr;
-    inf[LSM_INFO_DIST_TO_GOAL] = winfo[2 * N + i];
-    inf[LSM_INFO_TIME_REQ_TO_GOAL] = winfo[i];
-    inf[LSM_INFO_NUM_AGENT_COLLISIONS] = winfo[3 * N + i];
+    inf[LSM_INFO_DIST_TO_GOAL] = S.winfo[2 * N + i];
+    inf[LSM_INFO_TIME_REQ_TO_GOAL] = S.winfo[i];
+    inf[LSM_INFO_NUM_AGENT_COLLISIONS] = S.winfo[3 * N + i];
     inf[LSM_INFO_DISTANCE_MEAN] = dm;
     inf[LSM_INFO_DISTANCE_VARIANCE] = ds;
-    inf[LSM_INFO_DISTS_TRAVELED] = winfo[N + i];
+    inf[LSM_INFO_DISTS_TRAVELED] = S.winfo[N + i];
     inf[LSM_INFO_TIME_MEAN] = tm;
     inf[LSM_INFO_TIME_STDDEV] = ts;
-    inf[LSM_INFO_MIN_TIME_TO_GOAL] = P.s.gmt[(size_t)env * N + i];
-    inf[LSM_INFO_SAFETY_FILTERED] = (double)P.s.sfilt[(size_t)env * N + i];
+    inf[LSM_INFO_MIN_TIME_TO_GOAL] = S.gmt[i];
+    inf[LSM_INFO_SAFETY_FILTERED] = (double)S.sfilt[i];
     inf[LSM_INFO_SAFETY_VIOLATED] = (mr < S.cur[C_SEP]) ? 1.0 : 0.0;
-    inf[LSM_INFO_DECONFLICTING_INDEX] = (double)P.s.decon[(size_t)env * N + i];
-    inf[LSM_INFO_ACTION_DIFF] = P.s.adiff[(size_t)env * N + i];
+    inf[LSM_INFO_DECONFLICTING_INDEX] = (double)S.decon[i];
+    inf[LSM_INFO_ACTION_DIFF] = S.adiff[i];
     inf[LSM_INFO_REACHED_GOAL] = (double)S.rpost[i];
   }
+  STAMP(8);
 
   // ---- episode stats (environment.py:1004-1022), dones ---------------------------------
   bool my_done = true;
   if (lane < N) {
     const int i = lane;
-    double* stats = P.s.stats + (size_t)env * NSTAT * N;
     if (!S.dpost[i]) {  // departed is always True in the training scenario
-      stats[i] += 1;
+      S.stats[i] += 1;
       double vx, vy;
       agent_vel<DYN>(S, N, i, true, vx, vy);
-      stats[N + i] += blas_norm2(vx, vy) * P.dt;
+      S.stats[N + i] += blas_norm2(vx, vy) * P.dt;
+      const uint64_t m = S.emask[i];
       int cnt = 0, neng = 0;
       double mn = INFINITY;
-      const uint64_t m = ego_mask(S, N, P.L, i);
       for (int j = 0; j < N; ++j) {
         if (((m >> i) | (m >> j)) & 1ull) continue;
-        const double d = S.dist[i * E + j];
+        const double d = S.aa[i * N + j];
         if (!(d < P.coord_range && d > 0)) continue;
         cnt++;
         if (d < P.world_eng) neng++;
         mn = (d < mn) ? d : mn;
       }
       if (cnt > 0) {
-        if (neng > 1) stats[5 * N + i] += 1;
-        if (mn < P.sep_target) stats[3 * N + i] += 1;
-        if (mn < stats[4 * N + i]) stats[4 * N + i] = mn;
+        if (neng > 1) S.stats[5 * N + i] += 1;
+        if (mn < P.sep_target) S.stats[3 * N + i] += 1;
+        if (mn < S.stats[4 * N + i]) S.stats[4 * N + i] = mn;
       }
     }
-    if (S.dpost[i]) stats[2 * N + i] = 1;
+    if (S.dpost[i]) S.stats[2 * N + i] = 1;
     my_done = S.dpost[i] || cstep >= P.episode_length;
     P.o.dones[(size_t)env * N + i] = my_done ? 1 : 0;
   }
   const bool all_done = __all(my_done);
   __syncthreads();
+  STAMP(9);
 
-  // ---- 9. graph outputs, then optional auto-reset -----------------------------------------
+  // ---- 9. graph outputs, or the auto-reset (whose outputs replace them) ---------------------
   if (lane == 0) P.s.step[env] = cstep;
   if (P.auto_reset && all_done) {
     if (lane == 0) P.o.reset_flag[env] = 1;
     reset_env<DYN>(P, S, env);
     __syncthreads();
-    store_state<DYN>(P, S, env);
+    STAMP(12);
+    store_state<DYN>(P, S, env, true);
   } else {
     if (lane == 0) P.o.reset_flag[env] = 0;
     emit_graph<DYN>(P, S, env);
     __syncthreads();
-    store_state<DYN>(P, S, env);
+    STAMP(10);
+    store_state<DYN>(P, S, env, false);
   }
+  STAMP(11);
 }
 
 // env k's MT19937: np.random.seed(seed + 1000 * (env_offset + k))
@@ -1436,6 +1562,7 @@ static void fill_params(const lsm_env* e, KParams& P) {
   P.o.info = (double*)e->out_ptr[LSM_OUT_INFO];
   P.o.edges = (uint8_t*)e->out_ptr[LSM_OUT_EDGES];
   P.o.state = (double*)e->out_ptr[LSM_OUT_STATE];
+  P.stamps = (unsigned long long*)e->out_ptr[LSM_OUT_DEBUG_STAMPS];
 }
 
 extern "C" {
@@ -1453,6 +1580,7 @@ size_t lsm_output_bytes(const lsm_env* e, int32_t slot) {
     case LSM_OUT_INFO: return n * N * LSM_INFO_FIELDS * 8;
     case LSM_OUT_EDGES: return n * E * E;
     case LSM_OUT_STATE: return n * N * 4 * 8;
+    case LSM_OUT_DEBUG_STAMPS: return n * 16 * 8;
     default: return 0;
   }
 }
@@ -1622,7 +1750,7 @@ static int check_ready(lsm_env* e, bool stepping) {
 }
 
 static int launch(lsm_env* e, KParams& P, hipStream_t st) {
-  const size_t lds = lds_bytes(e->N, e->NL, e->E, e->F);
+  const size_t lds = lds_plan(e->N, e->NL, e->E, e->F).bytes;
   if (lds > 65536) return fail(e, "LDS footprint too large");
   if (P.dyn == 0)
     hipLaunchKernelGGL(rollout_kernel<0>, dim3(e->cfg.num_envs), dim3(WAVE), lds, st, P);

@@ -11,13 +11,13 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "csrc", "liblsm_rollout.so")
+LIB_PATH = os.environ.get("LSM_LIB") or os.path.join(os.path.dirname(_HERE), "csrc", "liblsm_rollout.so")
 
 LSM_DOUBLE_INTEGRATOR, LSM_AIRTAXI = 0, 1
 LSM_ACTIONS_INDEX_I32, LSM_ACTIONS_ONEHOT_F32, LSM_ACTIONS_ONEHOT_F64 = 0, 1, 2
 (OUT_OBS, OUT_NODE_OBS, OUT_ADJ, OUT_REWARD, OUT_DONE, OUT_RESET_FLAG, OUT_EP_INFO, OUT_INFO,
- OUT_EDGES, OUT_STATE) = range(10)
-NUM_OUT = 10
+ OUT_EDGES, OUT_STATE, OUT_DEBUG_STAMPS) = range(11)
+NUM_OUT = 11
 INFO_FIELDS = ("individual_reward", "min_relative_distance", "Dist_to_goal", "Time_req_to_goal",
                "Num_agent_collisions", "Distance_mean", "Distance_variance", "Dists_traveled",
                "Time_mean", "Time_stddev", "Min_time_to_goal", "Safety filtered", "Safety violated",

@@ -1,0 +1,77 @@
+"""Diagnostic: per-phase cycle breakdown of rollout_kernel from in-kernel s_memtime stamps.
+
+Uses a separate build (``-DLSM_STAMPS`` -> ``csrc/liblsm_rollout_stamps.so``); the
+product library never executes a stamp. Read the SHARES, not absolute times (the
+stamps' barriers forbid overlap the real kernel has).
+
+    python -m lsm.diag_stamps [--config 3] [--steps 40]
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(os.path.dirname(HERE), "csrc")
+STAMP_LIB = os.path.join(CSRC, "liblsm_rollout_stamps.so")
+PHASES = ["load", "decode", "filter-pairs", "filter-ego", "integrate", "dist+minrel", "obs+reward",
+          "info", "stats+dones", "emit-graph"]
+
+
+def build_stamps():
+    from . import build
+    cmd = [build.HIPCC] + build.FLAGS + ["-DLSM_STAMPS", "-o", STAMP_LIB, build.SRC]
+    subprocess.check_call(cmd, cwd=CSRC)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=40)
+    ap.add_argument("--build", action="store_true")
+    a = ap.parse_args()
+    if a.build or not os.path.exists(STAMP_LIB):
+        build_stamps()
+        if a.build:
+            return
+    os.environ["LSM_LIB"] = STAMP_LIB
+    import numpy as np
+    import torch
+    sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+    import bench
+    from . import capi, hj_tables
+    from .vec_env import GpuGraphVecEnv
+    import ctypes as C
+    c = bench.CONFIGS[a.config]
+    args = bench.make_args(c)
+    vt, tt = hj_tables.default_tables(c["dynamics_type"]) if (c["use_safety_filter"] or
+                                                              c["dynamics_type"] != "double_integrator") else (None, None)
+    env = GpuGraphVecEnv(args, num_envs=c["envs"], device="cuda:0", value_table=vt, ttr_table=tt,
+                         return_numpy=False, build_infos=False)
+    stamps = torch.zeros((c["envs"], 16), dtype=torch.int64, device="cuda:0")
+    capi.check(env.lib.lsm_bind_output(env.h, capi.OUT_DEBUG_STAMPS, C.c_void_p(stamps.data_ptr()),
+                                       stamps.numel() * 8), env.h)
+    env.reset(4)
+    N = c["num_agents"]
+    acc = []
+    for t in range(a.steps + 10):
+        act = torch.randint(0, 25, (c["envs"], N), device="cuda:0", dtype=torch.int32)
+        env.step(act, 4)
+        torch.cuda.synchronize()
+        if t >= 10:
+            s = stamps.cpu().numpy().astype(np.float64)
+            acc.append(np.diff(s[:, [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10]], axis=1))
+    d = np.concatenate(acc, axis=0)
+    med = np.median(d, axis=0)
+    tot = med.sum()
+    print("phase               median cycles   share")
+    for name, v in zip(PHASES, med):
+        print("%-18s %12.0f   %5.1f%%" % (name, v, 100 * v / tot))
+    print("%-18s %12.0f" % ("total", tot))
+    env.close()
+
+
+if __name__ == "__main__":
+    main()
