@@ -58,16 +58,21 @@ constexpr int NCUR = 12;
 constexpr int NSTAT = 6;        // travel_length, travel_distance, done, conflict, min_distance, multiple
 constexpr int NWINFO = 4;       // times_required, dists_to_goal, dist_left_to_goal, num_agent_collisions
 
+// HJ / TTR table in "cell-corner" layout: every grid cell stores the 2^ndim corner values
+// it interpolates (lexicographic corner order, dim 0 slowest) contiguously, so one query
+// reads 64 B (4-D) / 128 B (5-D) of values and 2^ndim * 16 * gw B of gradients -- one or
+// two cache lines instead of 2^ndim scattered nodes. 16x the node table (1.8 GB for the
+// full DI table): sized for 288 GB HBM, expanded on the device at upload.
 struct TableDev {
-  const float* values;
-  const float4* grads;
+  const float* cells;    // [n_cells][2^ndim]
+  const float4* gcells;  // [n_cells][2^ndim][gw]
   int ndim;
-  int n[5];
-  int stride[5];
+  int n[5];        // nodes per dim
+  int cstride[5];  // cell strides (cells per dim: n (periodic) or n - 1)
   float lo[5];
   float sp[5];
   int periodic[5];
-  int gw;  // float4 per node in grads (1 for <= 4 dims, 2 for 5 dims)
+  int gw;  // float4 per corner gradient (1 for <= 4 dims, 2 for 5 dims)
 };
 
 struct StateDev {
@@ -75,7 +80,7 @@ struct StateDev {
   double* pdist;     // [n][N]
   uint8_t* done;     // [n][N]
   int32_t* reached;  // [n][N]
-  double* lm;        // [n][4][NL]
+  double* lm;        // [n][6][NL] x, y, heading, speed, sin(heading), cos(heading)
   double* gmt;       // [n][N] goal_min_time
   int32_t* step;     // [n] env.current_step (== world.current_time_step)
   double* cur;       // [n][NCUR]
@@ -116,6 +121,7 @@ struct KParams {
   double cur_new[NCUR];
   uint32_t m_E, m_EE, m_EF, m_F;  // ceil(2^32 / d) for exact small-numerator division
   unsigned long long* stamps;     // LSM_OUT_DEBUG_STAMPS (diagnostic builds only)
+  const uint16_t* pairs;          // strict upper-triangle entity pairs (a | b << 8)
   TableDev val, ttr;
   StateDev s;
   OutDev o;
@@ -125,13 +131,13 @@ struct KParams {
 // ----------------------------------------------------------------------------------
 // LDS layout (dynamic, 16-byte aligned carve). Two unions keep one env under ~9 KB at
 // N = 8 so LDS does not cap residency below the VGPR limit (16 waves / CU):
-//   U1 = {fval, aa} (step)              | {mt, scen, scratch} (reset only)
-//   U2 = {dpair, vpair, inr} (filter)   | {feat, egooff} (DI outputs) | {stage} (airtaxi outputs)
+//   U1 = {fval, aa, aa2} (step)         | {mt, scen, scratch} (reset) | {stage} (node output, last)
+//   U2 = {dpair, vpair, inr} (filter)   | {feat, egooff} (DI node rows) | magnetic partial sums
 // ----------------------------------------------------------------------------------
 struct Lds {
   double* ps;        // [4][N] agent state (after integration; velocities pre-freeze)
-  double* lm;        // [4][NL]
-  double* lmsc;      // [2][NL] sin/cos of landmark headings
+  double* lm;        // [6][NL] x, y, heading, speed, sin, cos
+  double* lmsc;      // = lm + 4 NL
   double* raw;       // [2][N]
   double* safe;      // [2][N]
   int32_t* dpre;     // [N] done before reward update
@@ -153,6 +159,7 @@ struct Lds {
   // U1
   float* fval;       // [E][E] d if 0 < d < range else 0 (float32, unmasked)
   double* aa;        // [N][N] float64 agent-agent distances (episode stats)
+  double* aa2;       // [N][N] np.linalg.norm agent-agent distances (min relative distance, collisions)
   uint32_t* mt;      // [MT_WORDS]
   double* scen;      // [SCEN_WS]
   double* scratch;   // [2][MAXN]
@@ -181,25 +188,27 @@ __host__ __device__ inline LdsPlan lds_plan(int N, int NL, int E, int F) {
   size_t o = 0;
   int k = 0;
   auto put = [&](size_t bytes) { p.off[k++] = o; o += align16(bytes); };
-  put(8 * 4 * N); put(8 * 4 * NL); put(8 * 2 * NL); put(8 * 2 * N); put(8 * 2 * N);
+  put(8 * 4 * N); put(8 * 6 * NL); put(0); put(8 * 2 * N); put(8 * 2 * N);
   put(4 * N); put(4 * N); put(4 * N); put(4 * N);
   put(8 * N); put(8 * N); put(8 * NSTAT * N); put(8 * NWINFO * N); put(4 * N); put(4 * N);
   put(8 * N); put(8 * N); put(8 * 2 * N); put(8 * 2 * N); put(8 * NCUR); put(8 * N);
   // U1
   const size_t u1 = o;
-  size_t a = align16(4 * E * E), b = a + align16(8 * N * N);
+  size_t a = align16(4 * E * E), a2 = a + align16(8 * N * N), b = a2 + align16(8 * N * N);
   size_t c = align16(4 * MT_WORDS), d = c + align16(8 * SCEN_WS), e = d + align16(8 * 2 * MAXN);
-  p.off[k++] = u1; p.off[k++] = u1 + a; p.off[k++] = u1; p.off[k++] = u1 + c; p.off[k++] = u1 + d;
-  o = u1 + (b > e ? b : e);
+  p.off[k++] = u1; p.off[k++] = u1 + a; p.off[k++] = u1 + a2; p.off[k++] = u1; p.off[k++] = u1 + c;
+  p.off[k++] = u1 + d;
+  size_t u1sz = b > e ? b : e;
+  const size_t h0 = align16(4 * 64 * F);
+  u1sz = u1sz > h0 ? u1sz : h0;
+  o = u1 + u1sz;
   // U2
   const size_t u2 = o;
   size_t f1 = align16(8 * N * N), f2 = f1 + align16(4 * N * N), f3 = f2 + align16(N * N);
   size_t g1 = align16(8 * (2 * N + NL) * F), g2 = g1 + align16(8 * N * F);
-  size_t h1 = align16(4 * 64 * F);
   p.off[k++] = u2; p.off[k++] = u2 + f1; p.off[k++] = u2 + f2;
-  p.off[k++] = u2; p.off[k++] = u2 + g1; p.off[k++] = u2;
+  p.off[k++] = u2; p.off[k++] = u2 + g1; p.off[k++] = u1;   // stage aliases U1 (adj emitted first)
   size_t m = f3 > g2 ? f3 : g2;
-  m = m > h1 ? m : h1;
   m = m > (size_t)(8 * 2 * 64) ? m : (size_t)(8 * 2 * 64);   // magnetic partial sums (filter off)
   o = u2 + m;
   p.bytes = o;
@@ -212,7 +221,8 @@ __device__ __forceinline__ Lds carve(unsigned char* base, int N, int NL, int E, 
   int k = 0;
   L.ps = (double*)(base + p.off[k++]);
   L.lm = (double*)(base + p.off[k++]);
-  L.lmsc = (double*)(base + p.off[k++]);
+  L.lmsc = L.lm + 4 * NL;
+  k++;
   L.raw = (double*)(base + p.off[k++]);
   L.safe = (double*)(base + p.off[k++]);
   L.dpre = (int32_t*)(base + p.off[k++]);
@@ -233,6 +243,7 @@ __device__ __forceinline__ Lds carve(unsigned char* base, int N, int NL, int E, 
   L.emask = (uint64_t*)(base + p.off[k++]);
   L.fval = (float*)(base + p.off[k++]);
   L.aa = (double*)(base + p.off[k++]);
+  L.aa2 = (double*)(base + p.off[k++]);
   L.mt = (uint32_t*)(base + p.off[k++]);
   L.scen = (double*)(base + p.off[k++]);
   L.scratch = (double*)(base + p.off[k++]);
@@ -298,9 +309,9 @@ struct WaveRng {
 // HJ grid interpolation (float32; semantics of oracle/hj_grid.py)
 // ----------------------------------------------------------------------------------
 template <int ND>
-__device__ __forceinline__ bool grid_corners(const TableDev& T, const double* s, int* off, float* w) {
+__device__ __forceinline__ bool grid_cell(const TableDev& T, const double* s, int& cell, float* w) {
   float wl[ND], wh[ND];
-  int il[ND], ih[ND];
+  int il[ND];
 #pragma unroll
   for (int d = 0; d < ND; ++d) {
     float sd = (float)s[d];
@@ -313,31 +324,28 @@ __device__ __forceinline__ bool grid_corners(const TableDev& T, const double* s,
       wh[d] = p - (float)f;
       int a = f % n;
       if (a < 0) a += n;
-      int b = (f + 1) % n;
-      if (b < 0) b += n;
       il[d] = a;
-      ih[d] = b;
     } else {
       if (p < 0.0f || p > (float)(n - 1)) return false;
       if (f > n - 2) f = n - 2;
       wh[d] = p - (float)f;
       il[d] = f;
-      ih[d] = f + 1;
     }
     wl[d] = 1.0f - wh[d];
   }
+  int c0 = 0;
+#pragma unroll
+  for (int d = 0; d < ND; ++d) c0 += il[d] * T.cstride[d];
+  cell = c0;
 #pragma unroll
   for (int c = 0; c < (1 << ND); ++c) {
     float ww = 0.0f;
-    int o = 0;
 #pragma unroll
     for (int d = 0; d < ND; ++d) {
       const int bit = (c >> (ND - 1 - d)) & 1;
       const float wd = bit ? wh[d] : wl[d];
       ww = (d == 0) ? wd : ww * wd;
-      o += (bit ? ih[d] : il[d]) * T.stride[d];
     }
-    off[c] = o;
     w[c] = ww;
   }
   return true;
@@ -345,12 +353,16 @@ __device__ __forceinline__ bool grid_corners(const TableDev& T, const double* s,
 
 template <int ND>
 __device__ __forceinline__ bool interp_value(const TableDev& T, const double* s, float& out) {
-  int off[1 << ND];
+  int cell;
   float w[1 << ND];
-  if (!grid_corners<ND>(T, s, off, w)) return false;
+  if (!grid_cell<ND>(T, s, cell, w)) return false;
+  const float4* c4 = (const float4*)(T.cells + (size_t)cell * (1 << ND));
   float v[1 << ND];
 #pragma unroll
-  for (int c = 0; c < (1 << ND); ++c) v[c] = T.values[off[c]];
+  for (int q = 0; q < (1 << ND) / 4; ++q) {
+    const float4 x = c4[q];
+    v[4 * q] = x.x; v[4 * q + 1] = x.y; v[4 * q + 2] = x.z; v[4 * q + 3] = x.w;
+  }
   float acc = 0.0f;
 #pragma unroll
   for (int c = 0; c < (1 << ND); ++c) acc = acc + w[c] * v[c];
@@ -360,24 +372,52 @@ __device__ __forceinline__ bool interp_value(const TableDev& T, const double* s,
 
 template <int ND>
 __device__ __forceinline__ void interp_grad(const TableDev& T, const double* s, float* g) {
-  int off[1 << ND];
+  int cell;
   float w[1 << ND];
   for (int d = 0; d < ND; ++d) g[d] = 0.0f;
-  if (!grid_corners<ND>(T, s, off, w)) {
+  if (!grid_cell<ND>(T, s, cell, w)) {
     for (int d = 0; d < ND; ++d) g[d] = __builtin_nanf("");
     return;
   }
+  const float4* gc = T.gcells + (size_t)cell * (1 << ND) * T.gw;
 #pragma unroll
   for (int c = 0; c < (1 << ND); ++c) {
-    const float4 a = T.grads[(size_t)off[c] * T.gw];
+    const float4 a = gc[c * T.gw];
     float gv[8] = {a.x, a.y, a.z, a.w, 0.f, 0.f, 0.f, 0.f};
     if (ND > 4) {
-      const float4 b = T.grads[(size_t)off[c] * T.gw + 1];
+      const float4 b = gc[c * T.gw + 1];
       gv[4] = b.x; gv[5] = b.y; gv[6] = b.z; gv[7] = b.w;
     }
 #pragma unroll
     for (int d = 0; d < ND; ++d) g[d] = g[d] + w[c] * gv[d];
   }
+}
+
+// Expand a node table into the cell-corner layout (one thread per (cell, corner)).
+__global__ void expand_cells_kernel(const float* values, const float4* grads, float* cells, float4* gcells,
+                                    TableDev T, int64_t n_cells) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int nc = 1 << T.ndim;
+  if (t >= n_cells * nc) return;
+  const int64_t cell = t / nc;
+  const int c = (int)(t - cell * nc);
+  int64_t rem = cell, node = 0, nstride = 1;
+  int idx[5];
+  for (int d = T.ndim - 1; d >= 0; --d) {
+    const int ncd = T.periodic[d] ? T.n[d] : T.n[d] - 1;
+    idx[d] = (int)(rem % ncd);
+    rem /= ncd;
+  }
+  for (int d = T.ndim - 1; d >= 0; --d) {
+    const int bit = (c >> (T.ndim - 1 - d)) & 1;
+    int i = idx[d] + bit;
+    if (T.periodic[d] && i >= T.n[d]) i -= T.n[d];
+    node += (int64_t)i * nstride;
+    nstride *= T.n[d];
+  }
+  cells[t] = values[node];
+  if (grads)
+    for (int q = 0; q < T.gw; ++q) gcells[t * T.gw + q] = grads[node * T.gw + q];
 }
 
 // ----------------------------------------------------------------------------------
@@ -428,17 +468,15 @@ __device__ __forceinline__ double agent_theta(const Lds& S, int N, int j, bool p
   return S.ps[2 * N + j];
 }
 
-// evaluate_agent_goal_reached (navigation_graph_safe.py:606-656)
+// evaluate_agent_goal_reached (navigation_graph_safe.py:606-656) for goal gi, given the
+// agent's heading th, speed spd and he = direction_alignment_error(th, goal heading).
 template <int DYN>
-__device__ __forceinline__ bool goal_reached(const KParams& P, const Lds& S, int i, bool post, int reached) {
-  const int N = P.N, NL = P.NL;
-  const int gi = goal_index(reached, i, N, NL);
-  const double gx = S.lm[gi], gy = S.lm[NL + gi], gh = S.lm[2 * NL + gi], gs = S.lm[3 * NL + gi];
+__device__ __forceinline__ bool goal_reached_at(const Lds& S, int N, int NL, int i, int gi, double spd,
+                                                double he) {
+  const double gx = S.lm[gi], gy = S.lm[NL + gi], gs = S.lm[3 * NL + gi];
   const double px = S.ps[i], py = S.ps[N + i];
   const double dist = plain_norm2(px - gx, py - gy);
-  const double th = agent_theta<DYN>(S, N, i, post);
-  const double he = dae(th, gh);
-  const double verr = fabs(agent_speed<DYN>(S, N, i, post) - gs);
+  const double verr = fabs(spd - gs);
   const double mdt = S.cur[C_MDT], ghe = S.cur[C_GHE], gse = S.cur[C_GSE];
   bool cond;
   if (DYN == 0) {
@@ -843,78 +881,81 @@ __device__ __forceinline__ void build_rows_di(const KParams& P, Lds& S) {
   }
 }
 
-// node_obs [N][E][F] and adj [N][E][E] of one env (float4 stores when the env block is
-// 16-byte aligned). S.emask must hold the per-ego masks; S.fval the thresholded distances.
+// node_obs [N][E][F] and adj [N][E][E] of one env. Node rows are computed per (ego, entity)
+// pair by one lane, staged in LDS, and copied out as contiguous float4 when the env block is
+// 16-byte aligned; the adjacency is a masked select over the thresholded distance table,
+// one float4 (4 columns of one row) per lane-iteration when E % 4 == 0.
 template <int DYN>
 __device__ __forceinline__ void emit_graph(const KParams& P, Lds& S, int env) {
   const int lane = threadIdx.x;
   const int N = P.N, E = P.E, F = P.F;
   if (DYN == 0) build_rows_di(P, S);
   __syncthreads();
-  // ---- node features --------------------------------------------------------------
-  const int EF = E * F, ntot = N * EF;
-  float* node_out = P.o.node + (size_t)env * ntot;
-  if (DYN == 0) {
-    const bool vec = (ntot & 3) == 0;
-    const int step = vec ? 4 : 1;
-    for (int q0 = lane * step; q0 < ntot; q0 += WAVE * step) {
-      int e = fdiv(q0, P.m_EF);
-      const int rem = q0 - e * EF;
-      int k = fdiv(rem, P.m_F);
-      int f = rem - k * F;
-      float v[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        if (j < step) {
-          const int row = (k < N) ? ((k > e) ? k : N + k) : N + k;
-          v[j] = (float)(S.feat[row * F + f] - S.egooff[e * F + f]);
-          if (++f == F) { f = 0; if (++k == E) { k = 0; ++e; } }
-        }
-      }
-      if (vec) *(float4*)(node_out + q0) = make_float4(v[0], v[1], v[2], v[3]);
-      else node_out[q0] = v[0];
-    }
-  } else {
-    const int npairs = N * E;
-    for (int b0 = 0; b0 < npairs; b0 += WAVE) {
-      const int p = b0 + lane;
-      if (p < npairs) {
-        float f[11];
-        const int e = fdiv(p, P.m_E);
-        node_features<DYN>(P, S, e, p - e * E, f);
-        for (int q = 0; q < F; ++q) S.stage[lane * F + q] = f[q];
-      }
-      __syncthreads();
-      const int cnt = min(WAVE, npairs - b0) * F;
-      for (int q = lane; q < cnt; q += WAVE) node_out[(size_t)b0 * F + q] = S.stage[q];
-      __syncthreads();
-    }
-  }
   // ---- adjacency: ego e, row r, col c ------------------------------------------------------
   const int EE = E * E, atot = N * EE;
   float* adj_out = P.o.adj + (size_t)env * atot;
-  const bool vec = (atot & 3) == 0;
-  const int step = vec ? 4 : 1;
-  for (int q0 = lane * step; q0 < atot; q0 += WAVE * step) {
-    int e = fdiv(q0, P.m_EE);
-    const int u = q0 - e * EE;
-    int r = fdiv(u, P.m_E);
-    int c = u - r * E;
-    uint64_t m = S.emask[e];
-    float v[4];
+  if ((E & 3) == 0) {
+    for (int q0 = lane * 4; q0 < atot; q0 += WAVE * 4) {
+      const int e = fdiv(q0, P.m_EE);
+      const int u = q0 - e * EE;
+      const int r = fdiv(u, P.m_E);
+      const int c = u - r * E;
+      const uint64_t m = S.emask[e];
+      float4 v = *(const float4*)(S.fval + u);
+      if ((m >> r) & 1ull) {
+        v = make_float4(0.f, 0.f, 0.f, 0.f);
+      } else {
+        const uint32_t bits = (uint32_t)(m >> c) & 0xfu;
+        if (bits & 1u) v.x = 0.f;
+        if (bits & 2u) v.y = 0.f;
+        if (bits & 4u) v.z = 0.f;
+        if (bits & 8u) v.w = 0.f;
+      }
+      *(float4*)(adj_out + q0) = v;
+    }
+  } else {
+    for (int q = lane; q < atot; q += WAVE) {
+      const int e = fdiv(q, P.m_EE);
+      const int u = q - e * EE;
+      const int r = fdiv(u, P.m_E);
+      const int c = u - r * E;
+      const uint64_t m = S.emask[e];
+      adj_out[q] = (((m >> r) | (m >> c)) & 1ull) ? 0.0f : S.fval[u];
+    }
+  }
+  __syncthreads();   // fval dead from here: node staging reuses U1
+  // ---- node features --------------------------------------------------------------
+  const int npairs = N * E, ntot = npairs * F;
+  float* node_out = P.o.node + (size_t)env * ntot;
+  const bool nvec = (ntot & 3) == 0;
+  for (int b0 = 0; b0 < npairs; b0 += WAVE) {
+    const int p = b0 + lane;
+    if (p < npairs) {
+      const int e = fdiv(p, P.m_E);
+      const int k = p - e * E;
+      float* st = S.stage + lane * F;
+      if (DYN == 0) {
+        const int row = (k < N) ? ((k > e) ? k : N + k) : N + k;
+        const double* r = S.feat + row * F;
+        const double* o = S.egooff + e * F;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      if (j < step) {
-        const bool dis = (((m >> r) | (m >> c)) & 1ull) != 0;
-        v[j] = dis ? 0.0f : S.fval[r * E + c];
-        if (++c == E) {
-          c = 0;
-          if (++r == E) { r = 0; ++e; if (e < N) m = S.emask[e]; }
-        }
+        for (int q = 0; q < 10; ++q) st[q] = (float)(r[q] - o[q]);
+      } else {
+        float f[11];
+        node_features<DYN>(P, S, e, k, f);
+#pragma unroll
+        for (int q = 0; q < 11; ++q) st[q] = f[q];
       }
     }
-    if (vec) *(float4*)(adj_out + q0) = make_float4(v[0], v[1], v[2], v[3]);
-    else adj_out[q0] = v[0];
+    __syncthreads();
+    const int cnt = min(WAVE, npairs - b0) * F;
+    float* dst = node_out + (size_t)b0 * F;
+    if (nvec && (cnt & 3) == 0) {
+      for (int q = lane; q < cnt / 4; q += WAVE) ((float4*)dst)[q] = ((const float4*)S.stage)[q];
+    } else {
+      for (int q = lane; q < cnt; q += WAVE) dst[q] = S.stage[q];
+    }
+    __syncthreads();
   }
 }
 
@@ -923,20 +964,30 @@ __device__ __forceinline__ void emit_graph(const KParams& P, Lds& S, int env) {
 __device__ __forceinline__ void compute_dist(const KParams& P, Lds& S) {
   const int lane = threadIdx.x;
   const int N = P.N, E = P.E, NL = P.NL;
-  for (int u = lane; u < E * E; u += WAVE) {
-    const int a = fdiv(u, P.m_E), b = u - a * E;
-    double d = 0.0;
-    if (a != b) {
-      const int lo = a < b ? a : b, hi = a < b ? b : a;
-      const double xa = lo < N ? S.ps[lo] : S.lm[lo - N];
-      const double ya = lo < N ? S.ps[N + lo] : S.lm[NL + lo - N];
-      const double xb = hi < N ? S.ps[hi] : S.lm[hi - N];
-      const double yb = hi < N ? S.ps[N + hi] : S.lm[NL + hi - N];
-      const double dx = xa - xb, dy = ya - yb;
-      d = sqrt(dx * dx + dy * dy);
+  const int npair = E * (E - 1) / 2;
+  for (int t = lane; t < npair; t += WAVE) {
+    const uint32_t pr = P.pairs[t];
+    const int a = (int)(pr & 0xffu), b = (int)(pr >> 8);
+    const double xa = a < N ? S.ps[a] : S.lm[a - N];
+    const double ya = a < N ? S.ps[N + a] : S.lm[NL + a - N];
+    const double xb = b < N ? S.ps[b] : S.lm[b - N];
+    const double yb = b < N ? S.ps[N + b] : S.lm[NL + b - N];
+    const double dx = xa - xb, dy = ya - yb;
+    const double d = sqrt(dx * dx + dy * dy);   // |p_a - p_b| == |p_b - p_a| bit for bit
+    const float fv = (d < P.coord_range && d > 0) ? (float)d : 0.0f;
+    S.fval[a * E + b] = fv;
+    S.fval[b * E + a] = fv;
+    if (b < N) {
+      const double d2 = blas_norm2(dx, dy);
+      S.aa[a * N + b] = d;
+      S.aa[b * N + a] = d;
+      S.aa2[a * N + b] = d2;
+      S.aa2[b * N + a] = d2;
     }
-    S.fval[u] = (d < P.coord_range && d > 0) ? (float)d : 0.0f;
-    if (a < N && b < N) S.aa[a * N + b] = d;
+  }
+  for (int k = lane; k < E; k += WAVE) {
+    S.fval[k * E + k] = 0.0f;
+    if (k < N) { S.aa[k * N + k] = 0.0; S.aa2[k * N + k] = 0.0; }
   }
   __syncthreads();
 }
@@ -1068,7 +1119,7 @@ __device__ __forceinline__ void store_state(const KParams& P, const Lds& S, int 
     if (P.o.state) P.o.state[((size_t)env * N + j) * 4 + c] = v;
   }
   if (lm_changed)
-    for (int k = lane; k < 4 * NL; k += WAVE) P.s.lm[(size_t)env * 4 * NL + k] = S.lm[k];
+    for (int k = lane; k < 6 * NL; k += WAVE) P.s.lm[(size_t)env * 6 * NL + k] = S.lm[k];
   for (int k = lane; k < N; k += WAVE) {
     const size_t o = (size_t)env * N + k;
     P.s.done[o] = (uint8_t)S.dpost[k];
@@ -1095,7 +1146,7 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams P) {
 
   // ---- 0. one batch of coalesced loads of everything the env keeps in HBM ------------
   for (int k = lane; k < 4 * N; k += WAVE) S.ps[k] = P.s.st[(size_t)env * 4 * N + k];
-  for (int k = lane; k < 4 * NL; k += WAVE) S.lm[k] = P.s.lm[(size_t)env * 4 * NL + k];
+  for (int k = lane; k < 6 * NL; k += WAVE) S.lm[k] = P.s.lm[(size_t)env * 6 * NL + k];
   for (int k = lane; k < NSTAT * N; k += WAVE) S.stats[k] = P.s.stats[(size_t)env * NSTAT * N + k];
   for (int k = lane; k < NWINFO * N; k += WAVE) S.winfo[k] = P.s.winfo[(size_t)env * NWINFO * N + k];
   for (int k = lane; k < N; k += WAVE) {
@@ -1135,11 +1186,6 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams P) {
     __syncthreads();
     store_state<DYN>(P, S, env, true);
     return;
-  }
-
-  for (int k = lane; k < NL; k += WAVE) {
-    S.lmsc[k] = sin(S.lm[2 * NL + k]);
-    S.lmsc[NL + k] = cos(S.lm[2 * NL + k]);
   }
 
   // ---- 1. update_graph() at step start (previous state, final masks) --------------
@@ -1261,7 +1307,7 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams P) {
     if (!S.dpre[i]) {
       for (int j = 0; j < N; ++j) {
         if (j == i || S.dpre[j]) continue;
-        const double d = blas_norm2(S.ps[i] - S.ps[j], S.ps[N + i] - S.ps[N + j]);
+        const double d = S.aa2[i * N + j];
         m = (d < m) ? d : m;
       }
     }
@@ -1274,6 +1320,7 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams P) {
   if (DYN == 0 && !P.use_filter_arg) mag = magnetic_penalty_wave(P, S, S.dpair);
   double rew = 0.0;
   double th_pre = 0.0, spd_pre = 0.0;
+  bool reached_pre = false;
   if (lane < N) {
     const int i = lane;
     write_obs<DYN>(P, S, env, i);
@@ -1288,7 +1335,8 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams P) {
     const double se = fabs(spd - gs);
     const double sen = np_clip(se / S.cur[C_GSE], 0, 1);
     const double cra = P.use_filter_arg ? 1.0 : S.cur[C_RAT];
-    const bool reached = goal_reached<DYN>(P, S, i, false, S.rpre[i]);
+    const bool reached = goal_reached_at<DYN>(S, N, NL, i, gi, spd, he);
+    reached_pre = reached;
     const bool done0 = S.dpre[i] != 0;
     double r = 0.0;
     if (reached) {
@@ -1345,7 +1393,14 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams P) {
     const int gi = goal_index(S.rpost[i], i, N, NL);
     const double dist = plain_norm2(S.ps[i] - S.lm[gi], S.ps[N + i] - S.lm[NL + gi]);
     const double pd = S.pdist[i];
-    if (goal_reached<DYN>(P, S, i, true, S.rpost[i]) && tr == -1) {
+    bool reached_post = reached_pre;   // same state and goal unless the goal advanced
+    if (S.rpost[i] != S.rpre[i]) {
+      const bool frz = S.dpost[i] != 0;
+      const double thp = frz ? (DYN == 0 ? 0.0 : th_pre) : th_pre;   // atan2(0, 0) = 0
+      const double spp = frz ? 0.0 : spd_pre;
+      reached_post = goal_reached_at<DYN>(S, N, NL, i, gi, spp, dae(thp, S.lm[2 * NL + gi]));
+    }
+    if (reached_post && tr == -1) {
       tr = cstep * P.dt;
       dg = pd;
       dl = dist;
@@ -1357,7 +1412,7 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams P) {
     double nc = S.winfo[3 * N + i];
     for (int a = 0; a < N; ++a) {
       if (a == i) continue;
-      if (blas_norm2(S.ps[i] - S.ps[a], S.ps[N + i] - S.ps[N + a]) < 1.05 * (0.05 + 0.05)) nc += 1;
+      if (S.aa2[i * N + a] < 1.05 * (0.05 + 0.05)) nc += 1;
     }
     S.winfo[i] = tr; S.winfo[N + i] = dg; S.winfo[2 * N + i] = dl; S.winfo[3 * N + i] = nc;
     S.wnew[i] = dg; S.wnew[N + i] = tr;
@@ -1466,6 +1521,7 @@ using namespace lsm;
 
 struct lsm_env {
   lsm_config cfg;
+  uint16_t* pairs;
   int N, L, NL, E, F, OBS;
   StateDev s;
   std::vector<void*> allocs;
@@ -1563,6 +1619,7 @@ static void fill_params(const lsm_env* e, KParams& P) {
   P.o.edges = (uint8_t*)e->out_ptr[LSM_OUT_EDGES];
   P.o.state = (double*)e->out_ptr[LSM_OUT_STATE];
   P.stamps = (unsigned long long*)e->out_ptr[LSM_OUT_DEBUG_STAMPS];
+  P.pairs = e->pairs;
 }
 
 extern "C" {
@@ -1620,7 +1677,7 @@ int lsm_create(const lsm_config* cfg, lsm_env** out) {
   r |= dalloc(e, &e->s.pdist, n * N);
   r |= dalloc(e, &e->s.done, n * N);
   r |= dalloc(e, &e->s.reached, n * N);
-  r |= dalloc(e, &e->s.lm, n * 4 * e->NL);
+  r |= dalloc(e, &e->s.lm, n * 6 * e->NL);
   r |= dalloc(e, &e->s.gmt, n * N);
   r |= dalloc(e, &e->s.step, n);
   r |= dalloc(e, &e->s.cur, n * NCUR);
@@ -1632,12 +1689,20 @@ int lsm_create(const lsm_config* cfg, lsm_env** out) {
   r |= dalloc(e, &e->s.minrel, n * N);
   r |= dalloc(e, &e->s.adiff, n * N);
   r |= dalloc(e, &e->s.mt, n * MT_WORDS);
+  r |= dalloc(e, &e->pairs, (size_t)e->E * (e->E - 1) / 2 + 1);
   if (r) return 1;
+  {
+    std::vector<uint16_t> pr;
+    for (int a = 0; a < e->E; ++a)
+      for (int b = a + 1; b < e->E; ++b) pr.push_back((uint16_t)(a | (b << 8)));
+    pr.push_back(0);
+    HIPCHK(e, hipMemcpy(e->pairs, pr.data(), pr.size() * 2, hipMemcpyHostToDevice));
+  }
   HIPCHK(e, hipMemset(e->s.st, 0, n * 4 * N * 8));
   HIPCHK(e, hipMemset(e->s.pdist, 0, n * N * 8));
   HIPCHK(e, hipMemset(e->s.done, 0, n * N));
   HIPCHK(e, hipMemset(e->s.reached, 0, n * N * 4));
-  HIPCHK(e, hipMemset(e->s.lm, 0, n * 4 * e->NL * 8));
+  HIPCHK(e, hipMemset(e->s.lm, 0, n * 6 * e->NL * 8));
   HIPCHK(e, hipMemset(e->s.step, 0, n * 4));
   HIPCHK(e, hipMemset(e->s.cur, 0, n * NCUR * 8));
   HIPCHK(e, hipMemset(e->s.sfilt, 0, n * N));
@@ -1671,7 +1736,7 @@ int lsm_create(const lsm_config* cfg, lsm_env** out) {
 
 void lsm_destroy(lsm_env* e) {
   if (!e) return;
-  for (void* p : e->allocs) hipFree(p);
+  for (void* p : e->allocs) (void)hipFree(p);
   delete e;
 }
 
@@ -1681,33 +1746,46 @@ static int upload_table(lsm_env* e, TableDev& T, int32_t ndim, const double* lo,
   if (ndim < 1 || ndim > 5) return fail(e, "table ndim must be in [1, 5]");
   memset(&T, 0, sizeof(T));
   T.ndim = ndim;
-  size_t nodes = 1;
+  size_t nodes = 1, cells = 1;
   for (int d = 0; d < ndim; ++d) {
     if (shape[d] < 2) return fail(e, "table dims must have >= 2 nodes");
     nodes *= (size_t)shape[d];
+    cells *= (size_t)(periodic[d] ? shape[d] : shape[d] - 1);
   }
-  size_t stride = 1;
+  size_t cst = 1;
   for (int d = ndim - 1; d >= 0; --d) {
     T.n[d] = shape[d];
-    T.stride[d] = (int)stride;
-    stride *= shape[d];
+    T.cstride[d] = (int)cst;
+    cst *= (size_t)(periodic[d] ? shape[d] : shape[d] - 1);
     T.periodic[d] = periodic[d] ? 1 : 0;
     const double sp = T.periodic[d] ? (hi[d] - lo[d]) / shape[d] : (hi[d] - lo[d]) / (shape[d] - 1.0);
     T.lo[d] = (float)lo[d];
     T.sp[d] = (float)sp;
   }
-  if (nodes > (size_t)INT32_MAX) return fail(e, "table too large for 32-bit corner offsets");
+  const size_t ncorner = (size_t)1 << ndim;
+  if (cells * ncorner * 2 > (size_t)INT32_MAX) return fail(e, "table too large for 32-bit cell offsets");
+  T.gw = ndim <= 4 ? 1 : 2;
   float* dv = nullptr;
-  if (dalloc(e, &dv, nodes)) return 1;
+  float4* dg = nullptr;
+  HIPCHK(e, hipMalloc((void**)&dv, nodes * 4));
   HIPCHK(e, hipMemcpy(dv, values, nodes * 4, hipMemcpyHostToDevice));
-  T.values = dv;
   if (grads) {
-    T.gw = ndim <= 4 ? 1 : 2;
-    float4* dg = nullptr;
-    if (dalloc(e, &dg, nodes * T.gw)) return 1;
+    HIPCHK(e, hipMalloc((void**)&dg, nodes * T.gw * 16));
     HIPCHK(e, hipMemcpy(dg, grads, nodes * T.gw * 16, hipMemcpyHostToDevice));
-    T.grads = dg;
   }
+  float* cv = nullptr;
+  float4* cg = nullptr;
+  if (dalloc(e, &cv, cells * ncorner)) return 1;
+  if (grads && dalloc(e, &cg, cells * ncorner * T.gw)) return 1;
+  const int64_t work = (int64_t)(cells * ncorner);
+  hipLaunchKernelGGL(expand_cells_kernel, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, 0, dv, dg, cv, cg,
+                     T, (int64_t)cells);
+  HIPCHK(e, hipGetLastError());
+  HIPCHK(e, hipDeviceSynchronize());
+  HIPCHK(e, hipFree(dv));
+  if (dg) HIPCHK(e, hipFree(dg));
+  T.cells = cv;
+  T.gcells = cg;
   return 0;
 }
 
@@ -1717,7 +1795,7 @@ int lsm_set_value_table(lsm_env* e, int32_t ndim, const double* lo, const double
   if (ndim != want) return fail(e, "value table must be 4-D (double integrator) or 5-D (airtaxi)");
   if (!grads) return fail(e, "value table needs its gradient table");
   if (upload_table(e, e->val, ndim, lo, hi, shape, periodic, values, grads)) return 1;
-  e->tables_ok = (e->cfg.dynamics == LSM_DOUBLE_INTEGRATOR) || e->ttr.values != nullptr;
+  e->tables_ok = (e->cfg.dynamics == LSM_DOUBLE_INTEGRATOR) || e->ttr.cells != nullptr;
   return 0;
 }
 
@@ -1726,7 +1804,7 @@ int lsm_set_ttr_table(lsm_env* e, int32_t ndim, const double* lo, const double* 
   if (ndim != 4) return fail(e, "TTR table must be 4-D");
   if (upload_table(e, e->ttr, ndim, lo, hi, shape, periodic, values, nullptr)) return 1;
   e->ttr_max = ttr_max;
-  e->tables_ok = !e->cfg.use_safety_filter || e->val.values != nullptr;
+  e->tables_ok = !e->cfg.use_safety_filter || e->val.cells != nullptr;
   return 0;
 }
 
