@@ -96,7 +96,7 @@ def load_traffic(config, n_envs):
         return None
     try:
         d = json.load(open(p))
-        e = d.get(str(config))
+        e = d.get("config%d" % config)
         if e and int(e.get("num_envs", -1)) == n_envs:
             return float(e["hbm_bytes_per_launch"])
     except Exception:
@@ -142,12 +142,15 @@ def main():
                          env_offset=rank * n_envs, return_numpy=False, build_infos=False)
     N = c["num_agents"]
     gen = torch.Generator(device=dev).manual_seed(1234 + rank)
-    acts = torch.empty((n_envs, N), dtype=torch.int32, device=dev)
+    # Synthetic policy: every step's discrete actions drawn up front, resident in HBM before the
+    # timed region (the policy is outside the path; one env-step = one rollout_kernel launch).
+    acts_all = torch.randint(0, 25, (a.warmup + a.steps, n_envs, N), generator=gen, device=dev,
+                             dtype=torch.int32)
     env.reset(ep)
     epl = c["episode_length"]
 
     def one_step(t, ev=None):
-        torch.randint(0, 25, (n_envs, N), generator=gen, device=dev, dtype=torch.int32, out=acts)
+        acts = acts_all[t]
         if ev is not None:
             ev[0].record()
         env.step_async(acts, ep)
@@ -196,7 +199,7 @@ def main():
                        "hj_table": "synthetic %s" % (str(vt.shape) if vt is not None else "none"),
                        "parallelism": "env-sharded dp%d" % world},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
-                         "frac": achieved / PEAK_HBM_GBPS, "traffic": traffic,
+                         "frac": achieved / PEAK_HBM_GBPS, "traffic": traffic, "traffic_unit": "HBM bytes/launch (rocprofv3 PMC)",
                          "kernel": "rollout_kernel<%d>" % (0 if c["dynamics_type"] == "double_integrator" else 1),
                          "kernel_ms": kern_ms, "algorithmic_bytes_per_launch": bytes_launch,
                          "gather_bytes_per_launch": sb["gather_bytes"] * n_envs},

@@ -1,0 +1,100 @@
+"""Reduce rocprofv3 output of a bench run to the numbers the bench line cites.
+
+    python -m lsm.pmc stats  <kernel-trace dir>              -> per-kernel duration summary
+    python -m lsm.pmc traffic <fetch dir> <write dir> --config 3 --envs 4096 [--out profiles/pmc_traffic.json]
+
+``traffic`` reads the two separate PMC passes (FETCH_SIZE and WRITE_SIZE do not fit
+one TCC pass on gfx950) and applies the gfx950 corrections of
+/opt/skills/guides/MI355X_MICROARCH.md (HBM section): FETCH_SIZE is in KiB and
+counts half the bytes of wide coalesced reads (x2), WRITE_SIZE is exact for
+16-B/lane streaming stores.  Values are per launch of ``rollout_kernel``
+(mean over the profiled dispatches, warm-up launches excluded).
+"""
+from __future__ import annotations
+
+import argparse
+import csv
+import glob
+import json
+import os
+import statistics
+
+KERNEL = "rollout_kernel"
+
+
+def _rows(d, suffix):
+    files = glob.glob(os.path.join(d, "**", "*" + suffix), recursive=True)
+    if not files:
+        raise FileNotFoundError("no *%s under %s" % (suffix, d))
+    for f in files:
+        with open(f, newline="") as fh:
+            yield from csv.DictReader(fh)
+
+
+def counter_per_launch(d, counter, kernel=KERNEL, skip=5):
+    """Mean over dispatches of `kernel` of the counter summed over its instances."""
+    per = {}
+    for r in _rows(d, "counter_collection.csv"):
+        if kernel not in r.get("Kernel_Name", "") or r.get("Counter_Name") != counter:
+            continue
+        k = int(r.get("Dispatch_Id") or r.get("Correlation_Id") or 0)
+        per[k] = per.get(k, 0.0) + float(r["Counter_Value"])
+    vals = [per[k] for k in sorted(per)][skip:]
+    if not vals:
+        raise ValueError("counter %s not found for %s in %s" % (counter, kernel, d))
+    return statistics.fmean(vals), len(vals)
+
+
+def kernel_stats(d):
+    out = []
+    for r in _rows(d, "kernel_stats.csv"):
+        out.append({"name": r["Name"][:80], "calls": int(r["Calls"]),
+                    "avg_us": float(r["AverageNs"]) / 1e3, "pct": float(r["Percentage"])})
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    sub = ap.add_subparsers(dest="cmd", required=True)
+    s = sub.add_parser("stats")
+    s.add_argument("dir")
+    t = sub.add_parser("traffic")
+    t.add_argument("fetch_dir")
+    t.add_argument("write_dir")
+    t.add_argument("--config", type=int, required=True)
+    t.add_argument("--envs", type=int, required=True)
+    t.add_argument("--out", default=None)
+    c = sub.add_parser("counters")
+    c.add_argument("dirs", nargs="+")
+    a = ap.parse_args()
+    if a.cmd == "counters":
+        for d in a.dirs:
+            names = sorted({r["Counter_Name"] for r in _rows(d, "counter_collection.csv")})
+            for n in names:
+                v, k = counter_per_launch(d, n)
+                print("%-24s %16.1f  (mean of %d launches)" % (n, v, k))
+        return
+    if a.cmd == "stats":
+        for r in kernel_stats(a.dir):
+            print("%-80s %6d %10.2f us %6.2f%%" % (r["name"], r["calls"], r["avg_us"], r["pct"]))
+        return
+    fetch_kib, nf = counter_per_launch(a.fetch_dir, "FETCH_SIZE")
+    write_kib, nw = counter_per_launch(a.write_dir, "WRITE_SIZE")
+    rec = {"num_envs": a.envs, "fetch_size_kib_raw": fetch_kib, "write_size_kib": write_kib,
+           "fetch_bytes_corrected": 2 * fetch_kib * 1024, "write_bytes": write_kib * 1024,
+           "hbm_bytes_per_launch": 2 * fetch_kib * 1024 + write_kib * 1024,
+           "dispatches": [nf, nw],
+           "correction": "FETCH_SIZE x2 (gfx950, MI355X_MICROARCH.md HBM section); KiB -> bytes"}
+    print(json.dumps(rec))
+    if a.out:
+        db = {}
+        if os.path.exists(a.out):
+            with open(a.out) as fh:
+                db = json.load(fh)
+        db["config%d" % a.config] = rec
+        with open(a.out, "w") as fh:
+            json.dump(db, fh, indent=1, sort_keys=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -100,8 +100,8 @@ class GpuGraphVecEnv:
         self.t_node = torch.zeros((n, N, E, F), dtype=torch.float32, device=dev)
         self.t_adj = torch.zeros((n, N, E, E), dtype=torch.float32, device=dev)
         self.t_rew = torch.zeros((n, N), dtype=torch.float32, device=dev)
-        self.t_done = torch.zeros((n, N), dtype=torch.uint8, device=dev)
-        self.t_reset = torch.zeros((n,), dtype=torch.uint8, device=dev)
+        self.t_done = torch.zeros((n, N), dtype=torch.bool, device=dev)   # u8 buffer, 0/1
+        self.t_reset = torch.zeros((n,), dtype=torch.bool, device=dev)
         self.t_epinfo = torch.zeros((n, 8), dtype=torch.float64, device=dev)
         self.t_info = torch.zeros((n, N, len(capi.INFO_FIELDS)), dtype=torch.float64, device=dev)
         self.t_state = torch.zeros((n, N, 4), dtype=torch.float64, device=dev)
@@ -211,7 +211,7 @@ class GpuGraphVecEnv:
     def step_wait(self):
         self._pending = None
         if not self.return_numpy:
-            out = (self.t_obs, self.agent_id, self.t_node, self.t_adj, self.t_rew, self.t_done.bool(),
+            out = (self.t_obs, self.agent_id, self.t_node, self.t_adj, self.t_rew, self.t_done,
                    (self.t_info, self.t_reset, self.t_epinfo))
             return out + (0,) if not self.auto_reset else out
         obs = self.t_obs.cpu().numpy()
