@@ -26,6 +26,7 @@
 #include <math.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <string>
@@ -40,9 +41,17 @@
 #define STAMP(k)                                                                             \
   do {                                                                                       \
     __syncthreads();                                                                         \
-    if (threadIdx.x == 0 && P.stamps) P.stamps[(size_t)blockIdx.x * 16 + (k)] = __builtin_amdgcn_s_memtime(); \
+    if (lane == 0 && P.stamps) P.stamps[(size_t)env * 16 + (k)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+// slots 13/14: 100 MHz chip-wide clock at wave start / end (dispatch ramp and tail)
+#define RTSTAMP(k)                                                                           \
+  do {                                                                                       \
+    if (lane == 0 && P.stamps) P.stamps[(size_t)env * 16 + (k)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
 #else
+#define RTSTAMP(k) \
+  do {             \
+  } while (0)
 #define STAMP(k) \
   do {           \
   } while (0)
@@ -75,23 +84,20 @@ struct TableDev {
   int gw;  // float4 per corner gradient (1 for <= 4 dims, 2 for 5 dims)
 };
 
+// Persistent per-env state: ONE contiguous record per env (env-major, 128-B aligned
+// stride) whose byte layout is exactly the head of the env's LDS block (lds_plan), so a
+// step starts with a straight float4 copy HBM -> LDS (one round trip) and ends with the
+// copy back. Record fields in order (16-B aligned each): ps [4][N], stats [NSTAT][N],
+// winfo [NWINFO][N], pdist, gmt, minrel, adiff [N] f64, done, reached, sfilt, decon [N]
+// i32, step i32 | cur [NCUR] f64, lm [6][NL] f64 (x, y, heading, speed, sin, cos) -- the
+// part after '|' changes only at reset and is written back only then.
 struct StateDev {
-  double* st;        // [n][4][N]
-  double* pdist;     // [n][N]
-  uint8_t* done;     // [n][N]
-  int32_t* reached;  // [n][N]
-  double* lm;        // [n][6][NL] x, y, heading, speed, sin(heading), cos(heading)
-  double* gmt;       // [n][N] goal_min_time
-  int32_t* step;     // [n] env.current_step (== world.current_time_step)
-  double* cur;       // [n][NCUR]
-  double* stats;     // [n][NSTAT][N]
-  double* prev;      // [n][8]
-  double* winfo;     // [n][NWINFO][N]
-  uint8_t* sfilt;    // [n][N]  agent.safety_filtered
-  int32_t* decon;    // [n][N]  agent.deconflicting_agent_index
-  double* minrel;    // [n][N]  agent.min_relative_distance
-  double* adiff;     // [n][N]  agent.action_diff
-  uint32_t* mt;      // [n][MT_WORDS]
+  float4* rec;          // [n][rec_stride16]
+  uint32_t rec_stride16;
+  uint32_t rec16;       // float4 per record
+  uint32_t hot16;       // float4 rewritten every step (up to cur)
+  double* prev;         // [n][8] previous episode summary
+  uint32_t* mt;         // [n][MT_WORDS]
 };
 
 struct OutDev {
@@ -121,6 +127,7 @@ struct KParams {
   double cur_new[NCUR];
   uint32_t m_E, m_EE, m_EF, m_F;  // ceil(2^32 / d) for exact small-numerator division
   unsigned long long* stamps;     // LSM_OUT_DEBUG_STAMPS (diagnostic builds only)
+  uint32_t lds_env_bytes;         // LDS bytes per env (envs per wave > 1: consecutive blocks)
   const uint16_t* pairs;          // strict upper-triangle entity pairs (a | b << 8)
   TableDev val, ttr;
   StateDev s;
@@ -135,26 +142,29 @@ struct KParams {
 //   U2 = {dpair, vpair, inr} (filter)   | {feat, egooff} (DI node rows) | magnetic partial sums
 // ----------------------------------------------------------------------------------
 struct Lds {
+  // ---- persistent record (StateDev) ----
   double* ps;        // [4][N] agent state (after integration; velocities pre-freeze)
-  double* lm;        // [6][NL] x, y, heading, speed, sin, cos
-  double* lmsc;      // = lm + 4 NL
-  double* raw;       // [2][N]
-  double* safe;      // [2][N]
-  int32_t* dpre;     // [N] done before reward update
-  int32_t* dpost;    // [N] done after
-  int32_t* rpre;     // [N] reached_goal before
-  int32_t* rpost;    // [N] reached_goal after
-  double* pdist;     // [N] travel distance (state.p_dist)
-  double* gmt;       // [N] goal_min_time
   double* stats;     // [NSTAT][N]
   double* winfo;     // [NWINFO][N]
-  int32_t* sfilt;    // [N]
-  int32_t* decon;    // [N]
+  double* pdist;     // [N] travel distance (state.p_dist)
+  double* gmt;       // [N] goal_min_time
   double* minrel;    // [N]
   double* adiff;     // [N]
+  int32_t* dpost;    // [N] done after the reward update (record: done)
+  int32_t* rpost;    // [N] reached_goal after (record: reached)
+  int32_t* sfilt;    // [N]
+  int32_t* decon;    // [N]
+  int32_t* step;     // [1] env.current_step
+  double* cur;       // [NCUR]
+  double* lm;        // [6][NL] x, y, heading, speed, sin, cos
+  double* lmsc;      // = lm + 4 NL
+  // ---- step scratch ----
+  int32_t* dpre;     // [N] done before reward update
+  int32_t* rpre;     // [N] reached_goal before
+  double* raw;       // [2][N]
+  double* safe;      // [2][N]
   double* wold;      // [2][N] dists_to_goal / times_required before this step's info
   double* wnew;      // [2][N] after
-  double* cur;       // [NCUR]
   uint64_t* emask;   // [N] bit r: entity r disconnected for ego e (snapshot rule)
   // U1
   float* fval;       // [E][E] d if 0 < d < range else 0 (float32, unmasked)
@@ -173,7 +183,9 @@ struct Lds {
 };
 
 struct LdsPlan {
-  size_t bytes;
+  size_t bytes;     // LDS per env
+  size_t rec;       // persistent record bytes (LDS head == HBM record)
+  size_t hot;       // record bytes rewritten every step (fields before cur)
   size_t off[40];
 };
 
@@ -182,16 +194,21 @@ __device__ __forceinline__ int fdiv(int q, uint32_t m) { return (int)__umulhi((u
 
 __host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
 
-// Offsets of every LDS array (shared by the host launch and the device carve).
+// Offsets of every LDS array (shared by the host launch/record init and the device carve).
 __host__ __device__ inline LdsPlan lds_plan(int N, int NL, int E, int F) {
   LdsPlan p;
   size_t o = 0;
   int k = 0;
   auto put = [&](size_t bytes) { p.off[k++] = o; o += align16(bytes); };
-  put(8 * 4 * N); put(8 * 6 * NL); put(0); put(8 * 2 * N); put(8 * 2 * N);
-  put(4 * N); put(4 * N); put(4 * N); put(4 * N);
-  put(8 * N); put(8 * N); put(8 * NSTAT * N); put(8 * NWINFO * N); put(4 * N); put(4 * N);
-  put(8 * N); put(8 * N); put(8 * 2 * N); put(8 * 2 * N); put(8 * NCUR); put(8 * N);
+  // record
+  put(8 * 4 * N); put(8 * NSTAT * N); put(8 * NWINFO * N);
+  put(8 * N); put(8 * N); put(8 * N); put(8 * N);
+  put(4 * N); put(4 * N); put(4 * N); put(4 * N); put(4);
+  p.hot = o;
+  put(8 * NCUR); put(8 * 6 * NL);
+  p.rec = o;
+  // scratch
+  put(4 * N); put(4 * N); put(8 * 2 * N); put(8 * 2 * N); put(8 * 2 * N); put(8 * 2 * N); put(8 * N);
   // U1
   const size_t u1 = o;
   size_t a = align16(4 * E * E), a2 = a + align16(8 * N * N), b = a2 + align16(8 * N * N);
@@ -199,7 +216,7 @@ __host__ __device__ inline LdsPlan lds_plan(int N, int NL, int E, int F) {
   p.off[k++] = u1; p.off[k++] = u1 + a; p.off[k++] = u1 + a2; p.off[k++] = u1; p.off[k++] = u1 + c;
   p.off[k++] = u1 + d;
   size_t u1sz = b > e ? b : e;
-  const size_t h0 = align16(4 * 64 * F);
+  const size_t h0 = align16(4 * WAVE * F);   // node staging for up to 64 pairs
   u1sz = u1sz > h0 ? u1sz : h0;
   o = u1 + u1sz;
   // U2
@@ -220,26 +237,26 @@ __device__ __forceinline__ Lds carve(unsigned char* base, int N, int NL, int E, 
   Lds L;
   int k = 0;
   L.ps = (double*)(base + p.off[k++]);
-  L.lm = (double*)(base + p.off[k++]);
-  L.lmsc = L.lm + 4 * NL;
-  k++;
-  L.raw = (double*)(base + p.off[k++]);
-  L.safe = (double*)(base + p.off[k++]);
-  L.dpre = (int32_t*)(base + p.off[k++]);
-  L.dpost = (int32_t*)(base + p.off[k++]);
-  L.rpre = (int32_t*)(base + p.off[k++]);
-  L.rpost = (int32_t*)(base + p.off[k++]);
-  L.pdist = (double*)(base + p.off[k++]);
-  L.gmt = (double*)(base + p.off[k++]);
   L.stats = (double*)(base + p.off[k++]);
   L.winfo = (double*)(base + p.off[k++]);
-  L.sfilt = (int32_t*)(base + p.off[k++]);
-  L.decon = (int32_t*)(base + p.off[k++]);
+  L.pdist = (double*)(base + p.off[k++]);
+  L.gmt = (double*)(base + p.off[k++]);
   L.minrel = (double*)(base + p.off[k++]);
   L.adiff = (double*)(base + p.off[k++]);
+  L.dpost = (int32_t*)(base + p.off[k++]);
+  L.rpost = (int32_t*)(base + p.off[k++]);
+  L.sfilt = (int32_t*)(base + p.off[k++]);
+  L.decon = (int32_t*)(base + p.off[k++]);
+  L.step = (int32_t*)(base + p.off[k++]);
+  L.cur = (double*)(base + p.off[k++]);
+  L.lm = (double*)(base + p.off[k++]);
+  L.lmsc = L.lm + 4 * NL;
+  L.dpre = (int32_t*)(base + p.off[k++]);
+  L.rpre = (int32_t*)(base + p.off[k++]);
+  L.raw = (double*)(base + p.off[k++]);
+  L.safe = (double*)(base + p.off[k++]);
   L.wold = (double*)(base + p.off[k++]);
   L.wnew = (double*)(base + p.off[k++]);
-  L.cur = (double*)(base + p.off[k++]);
   L.emask = (uint64_t*)(base + p.off[k++]);
   L.fval = (float*)(base + p.off[k++]);
   L.aa = (double*)(base + p.off[k++]);
@@ -261,13 +278,14 @@ enum { C_CR = 0, C_SLOPED, C_STAIR, C_RAT, C_RSC, C_GHE, C_GSE, C_MDT, C_SEP, C_
 // ----------------------------------------------------------------------------------
 // Wave-cooperative MT19937 (numpy legacy stream); all lanes run the same scalar sequence.
 // ----------------------------------------------------------------------------------
+template <int LPE>
 struct WaveRng {
   uint32_t* key;
   int pos;
   __device__ __forceinline__ void gen() {
-    const int lane = threadIdx.x;
+    const int lane = threadIdx.x & (LPE - 1);
     // phase A: i in [0, 227) reads old key[i], key[i+1], key[i+397]
-    for (int base = 0; base < MT_N - MT_M; base += WAVE) {
+    for (int base = 0; base < MT_N - MT_M; base += LPE) {
       int i = base + lane;
       uint32_t v = 0;
       if (i < MT_N - MT_M) v = mt_twist1(key[i], key[i + 1], key[i + MT_M]);
@@ -276,7 +294,7 @@ struct WaveRng {
       __syncthreads();
     }
     // phases B, C: i in [227, 623) reads new key[i-227]
-    for (int base = MT_N - MT_M; base < MT_N - 1; base += WAVE) {
+    for (int base = MT_N - MT_M; base < MT_N - 1; base += LPE) {
       int i = base + lane;
       uint32_t v = 0;
       if (i < MT_N - 1) v = mt_twist1(key[i], key[i + 1], key[i + (MT_M - MT_N)]);
@@ -503,11 +521,12 @@ __device__ __forceinline__ bool goal_reached_at(const Lds& S, int N, int NL, int
 // the G partial sums are combined in lane order (float64; ulp-level vs the reference's
 // sequential sum, reward tolerance). Called by ALL lanes; returns the penalty in lanes
 // lane < N (agent = lane), garbage elsewhere.
+template <int LPE>
 __device__ __forceinline__ double magnetic_penalty_wave(const KParams& P, Lds& S, double* part) {
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & (LPE - 1);
   const int N = P.N, NL = P.NL;
   int G = 1;
-  while (G * 2 * N <= WAVE) G *= 2;
+  while (G * 2 * N <= LPE) G *= 2;
   const int a = lane / G, g = lane - a * G;
   const bool act = a < N;
   const int ai = act ? a : 0;
@@ -536,7 +555,7 @@ __device__ __forceinline__ double magnetic_penalty_wave(const KParams& P, Lds& S
     }
   }
   part[lane] = m0;
-  part[WAVE + lane] = m1;
+  part[LPE + lane] = m1;
   __syncthreads();
   double pen = 0.0;
   if (lane < N) {
@@ -554,7 +573,7 @@ __device__ __forceinline__ double magnetic_penalty_wave(const KParams& P, Lds& S
       double s0 = 0.0, s1 = 0.0;
       for (int q = 0; q < G; ++q) {
         s0 += part[i * G + q];
-        s1 += part[WAVE + i * G + q];
+        s1 += part[LPE + i * G + q];
       }
       s0 = s0 / 0.5;
       href = atan2(s1, s0);
@@ -850,10 +869,11 @@ __device__ __forceinline__ uint64_t ego_mask(const Lds& S, int N, int L, int e) 
 
 // DI node features are (entity row) - (ego offset): rows for agents (pre, post update) and
 // landmarks, offsets per ego, built once per step in LDS (utils.py:201-255).
+template <int LPE>
 __device__ __forceinline__ void build_rows_di(const KParams& P, Lds& S) {
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & (LPE - 1);
   const int N = P.N, NL = P.NL, F = P.F;
-  for (int t = lane; t < 2 * N + NL; t += WAVE) {
+  for (int t = lane; t < 2 * N + NL; t += LPE) {
     double* r = S.feat + (size_t)t * F;
     if (t < 2 * N) {
       const bool post = t >= N;
@@ -885,17 +905,17 @@ __device__ __forceinline__ void build_rows_di(const KParams& P, Lds& S) {
 // pair by one lane, staged in LDS, and copied out as contiguous float4 when the env block is
 // 16-byte aligned; the adjacency is a masked select over the thresholded distance table,
 // one float4 (4 columns of one row) per lane-iteration when E % 4 == 0.
-template <int DYN>
+template <int DYN, int LPE>
 __device__ __forceinline__ void emit_graph(const KParams& P, Lds& S, int env) {
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & (LPE - 1);
   const int N = P.N, E = P.E, F = P.F;
-  if (DYN == 0) build_rows_di(P, S);
+  if (DYN == 0) build_rows_di<LPE>(P, S);
   __syncthreads();
   // ---- adjacency: ego e, row r, col c ------------------------------------------------------
   const int EE = E * E, atot = N * EE;
   float* adj_out = P.o.adj + (size_t)env * atot;
   if ((E & 3) == 0) {
-    for (int q0 = lane * 4; q0 < atot; q0 += WAVE * 4) {
+    for (int q0 = lane * 4; q0 < atot; q0 += LPE * 4) {
       const int e = fdiv(q0, P.m_EE);
       const int u = q0 - e * EE;
       const int r = fdiv(u, P.m_E);
@@ -914,7 +934,7 @@ __device__ __forceinline__ void emit_graph(const KParams& P, Lds& S, int env) {
       *(float4*)(adj_out + q0) = v;
     }
   } else {
-    for (int q = lane; q < atot; q += WAVE) {
+    for (int q = lane; q < atot; q += LPE) {
       const int e = fdiv(q, P.m_EE);
       const int u = q - e * EE;
       const int r = fdiv(u, P.m_E);
@@ -928,7 +948,7 @@ __device__ __forceinline__ void emit_graph(const KParams& P, Lds& S, int env) {
   const int npairs = N * E, ntot = npairs * F;
   float* node_out = P.o.node + (size_t)env * ntot;
   const bool nvec = (ntot & 3) == 0;
-  for (int b0 = 0; b0 < npairs; b0 += WAVE) {
+  for (int b0 = 0; b0 < npairs; b0 += LPE) {
     const int p = b0 + lane;
     if (p < npairs) {
       const int e = fdiv(p, P.m_E);
@@ -948,12 +968,12 @@ __device__ __forceinline__ void emit_graph(const KParams& P, Lds& S, int env) {
       }
     }
     __syncthreads();
-    const int cnt = min(WAVE, npairs - b0) * F;
+    const int cnt = min(LPE, npairs - b0) * F;
     float* dst = node_out + (size_t)b0 * F;
     if (nvec && (cnt & 3) == 0) {
-      for (int q = lane; q < cnt / 4; q += WAVE) ((float4*)dst)[q] = ((const float4*)S.stage)[q];
+      for (int q = lane; q < cnt / 4; q += LPE) ((float4*)dst)[q] = ((const float4*)S.stage)[q];
     } else {
-      for (int q = lane; q < cnt; q += WAVE) dst[q] = S.stage[q];
+      for (int q = lane; q < cnt; q += LPE) dst[q] = S.stage[q];
     }
     __syncthreads();
   }
@@ -961,11 +981,12 @@ __device__ __forceinline__ void emit_graph(const KParams& P, Lds& S, int env) {
 
 // cached_dist_mag (core.py:514-543): float32 thresholded copy for the adjacency
 // (adj = d * (d < range) * (d > 0), navigation_graph_safe.py:991-992) + float64 agent block.
+template <int LPE>
 __device__ __forceinline__ void compute_dist(const KParams& P, Lds& S) {
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & (LPE - 1);
   const int N = P.N, E = P.E, NL = P.NL;
   const int npair = E * (E - 1) / 2;
-  for (int t = lane; t < npair; t += WAVE) {
+  for (int t = lane; t < npair; t += LPE) {
     const uint32_t pr = P.pairs[t];
     const int a = (int)(pr & 0xffu), b = (int)(pr >> 8);
     const double xa = a < N ? S.ps[a] : S.lm[a - N];
@@ -985,7 +1006,7 @@ __device__ __forceinline__ void compute_dist(const KParams& P, Lds& S) {
       S.aa2[b * N + a] = d2;
     }
   }
-  for (int k = lane; k < E; k += WAVE) {
+  for (int k = lane; k < E; k += LPE) {
     S.fval[k * E + k] = 0.0f;
     if (k < N) { S.aa[k * N + k] = 0.0; S.aa2[k * N + k] = 0.0; }
   }
@@ -1052,9 +1073,9 @@ __device__ __forceinline__ void summary(const KParams& P, const Lds& S, double* 
 
 // Device reset of one env (MultiAgentGraphEnv.reset, environment.py:1046-1074). Expects the
 // env's persistent per-agent arrays in LDS (S.stats, S.rpost = reached_goal before reset).
-template <int DYN>
+template <int DYN, int LPE>
 __device__ __forceinline__ void reset_env(const KParams& P, Lds& S, int env) {
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & (LPE - 1);
   const int N = P.N, NL = P.NL;
   double* prev = P.s.prev + (size_t)env * 8;
   if (lane == 0) {
@@ -1066,14 +1087,11 @@ __device__ __forceinline__ void reset_env(const KParams& P, Lds& S, int env) {
     }
   }
   __syncthreads();
-  for (int k = lane; k < NCUR; k += WAVE) {
-    S.cur[k] = P.cur_new[k];
-    P.s.cur[(size_t)env * NCUR + k] = P.cur_new[k];
-  }
+  for (int k = lane; k < NCUR; k += LPE) S.cur[k] = P.cur_new[k];
   const uint32_t* mtg = P.s.mt + (size_t)env * MT_WORDS;
-  for (int k = lane; k < MT_WORDS; k += WAVE) S.mt[k] = mtg[k];
+  for (int k = lane; k < MT_WORDS; k += LPE) S.mt[k] = mtg[k];
   __syncthreads();
-  WaveRng rng;
+  WaveRng<LPE> rng;
   rng.key = S.mt;
   rng.pos = (int)S.mt[MT_N];
   ScenarioParams sp;
@@ -1086,12 +1104,12 @@ __device__ __forceinline__ void reset_env(const KParams& P, Lds& S, int env) {
   if (lane == 0) S.mt[MT_N] = (uint32_t)rng.pos;
   __syncthreads();
   uint32_t* mtw = P.s.mt + (size_t)env * MT_WORDS;
-  for (int k = lane; k < MT_WORDS; k += WAVE) mtw[k] = S.mt[k];
-  for (int k = lane; k < NL; k += WAVE) {
+  for (int k = lane; k < MT_WORDS; k += LPE) mtw[k] = S.mt[k];
+  for (int k = lane; k < NL; k += LPE) {
     S.lmsc[k] = sin(S.lm[2 * NL + k]);
     S.lmsc[NL + k] = cos(S.lm[2 * NL + k]);
   }
-  for (int k = lane; k < N; k += WAVE) {
+  for (int k = lane; k < N; k += LPE) {
     S.dpre[k] = 0; S.dpost[k] = 0; S.rpre[k] = 0; S.rpost[k] = 0;
     S.emask[k] = 0;
     S.winfo[k] = -1.0; S.winfo[N + k] = -1.0; S.winfo[2 * N + k] = -1.0; S.winfo[3 * N + k] = 0.0;
@@ -1099,69 +1117,65 @@ __device__ __forceinline__ void reset_env(const KParams& P, Lds& S, int env) {
     S.pdist[k] = 0.0;
     S.gmt[k] = plain_norm2(S.ps[k] - S.lm[k], S.ps[N + k] - S.lm[NL + k]) / P.max_speed;
   }
-  if (lane == 0) P.s.step[env] = 0;
+  if (lane == 0) S.step[0] = 0;
   __syncthreads();   // MT words read out of U1 before compute_dist overwrites it
-  compute_dist(P, S);
+  compute_dist<LPE>(P, S);
   if (lane < N) write_obs<DYN>(P, S, env, lane);
-  emit_graph<DYN>(P, S, env);
+  emit_graph<DYN, LPE>(P, S, env);
 }
 
-// Persistent per-env arrays: LDS -> HBM.
-template <int DYN>
-__device__ __forceinline__ void store_state(const KParams& P, const Lds& S, int env, bool lm_changed) {
-  const int lane = threadIdx.x;
-  const int N = P.N, NL = P.NL;
-  for (int k = lane; k < 4 * N; k += WAVE) {
+// Record copy between HBM and the head of the env's LDS block: up to 4 float4 per lane in
+// flight before the first write, so a record of <= 4 KB costs one round trip.
+template <int LPE>
+__device__ __forceinline__ void rec_copy(const float4* src, float4* dst, int n16) {
+  const int lane = threadIdx.x & (LPE - 1);
+  for (int k0 = lane; k0 < n16; k0 += 4 * LPE) {
+    const int k1 = k0 + LPE, k2 = k0 + 2 * LPE, k3 = k0 + 3 * LPE;
+    const int last = n16 - 1;   // clamped (always in-bounds) loads, predicated stores
+    const float4 r0 = src[k0];
+    const float4 r1 = src[k1 < last ? k1 : last];
+    const float4 r2 = src[k2 < last ? k2 : last];
+    const float4 r3 = src[k3 < last ? k3 : last];
+    dst[k0] = r0;
+    if (k1 < n16) dst[k1] = r1;
+    if (k2 < n16) dst[k2] = r2;
+    if (k3 < n16) dst[k3] = r3;
+  }
+}
+
+// Persistent record: LDS -> HBM (done agents' velocity / speed stored as zero, core.py
+// freezes them). `full` also writes cur + landmarks (after a reset).
+template <int DYN, int LPE>
+__device__ __forceinline__ void store_state(const KParams& P, Lds& S, const unsigned char* lbase, int env,
+                                            bool full) {
+  const int lane = threadIdx.x & (LPE - 1);
+  const int N = P.N;
+  for (int k = lane; k < 4 * N; k += LPE) {
     const int c = k / N, j = k - c * N;
     double v = S.ps[k];
     if (S.dpost[j] && (DYN == 0 ? (c >= 2) : (c == 3))) v = 0.0;
-    P.s.st[(size_t)env * 4 * N + k] = v;
+    S.ps[k] = v;
     if (P.o.state) P.o.state[((size_t)env * N + j) * 4 + c] = v;
   }
-  if (lm_changed)
-    for (int k = lane; k < 6 * NL; k += WAVE) P.s.lm[(size_t)env * 6 * NL + k] = S.lm[k];
-  for (int k = lane; k < N; k += WAVE) {
-    const size_t o = (size_t)env * N + k;
-    P.s.done[o] = (uint8_t)S.dpost[k];
-    P.s.reached[o] = S.rpost[k];
-    P.s.pdist[o] = S.pdist[k];
-    P.s.gmt[o] = S.gmt[k];
-    P.s.sfilt[o] = (uint8_t)S.sfilt[k];
-    P.s.decon[o] = S.decon[k];
-    P.s.minrel[o] = S.minrel[k];
-    P.s.adiff[o] = S.adiff[k];
-  }
-  for (int k = lane; k < NSTAT * N; k += WAVE) P.s.stats[(size_t)env * NSTAT * N + k] = S.stats[k];
-  for (int k = lane; k < NWINFO * N; k += WAVE) P.s.winfo[(size_t)env * NWINFO * N + k] = S.winfo[k];
+  __syncthreads();
+  rec_copy<LPE>((const float4*)lbase, P.s.rec + (size_t)env * P.s.rec_stride16, full ? P.s.rec16 : P.s.hot16);
 }
 
-template <int DYN>
+template <int DYN, int LPE>
 __global__ __launch_bounds__(64) void rollout_kernel(const KParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int env = blockIdx.x;
-  const int lane = threadIdx.x;
+  constexpr int G = WAVE / LPE;   // envs per wave, one per LPE-lane group
+  const int grp = (G == 1) ? 0 : (int)threadIdx.x / LPE;
+  const int env = blockIdx.x * G + grp;
+  const int lane = threadIdx.x & (LPE - 1);
+  if (env >= P.n_envs) return;
   const int N = P.N, NL = P.NL, E = P.E;
-  Lds S = carve(smem, N, NL, E, P.F);
+  unsigned char* lbase = smem + (size_t)grp * P.lds_env_bytes;
+  Lds S = carve(lbase, N, NL, E, P.F);
+  RTSTAMP(13);
   STAMP(0);
 
-  // ---- 0. one batch of coalesced loads of everything the env keeps in HBM ------------
-  for (int k = lane; k < 4 * N; k += WAVE) S.ps[k] = P.s.st[(size_t)env * 4 * N + k];
-  for (int k = lane; k < 6 * NL; k += WAVE) S.lm[k] = P.s.lm[(size_t)env * 6 * NL + k];
-  for (int k = lane; k < NSTAT * N; k += WAVE) S.stats[k] = P.s.stats[(size_t)env * NSTAT * N + k];
-  for (int k = lane; k < NWINFO * N; k += WAVE) S.winfo[k] = P.s.winfo[(size_t)env * NWINFO * N + k];
-  for (int k = lane; k < N; k += WAVE) {
-    const size_t o = (size_t)env * N + k;
-    const int d = P.s.done[o];
-    const int r = P.s.reached[o];
-    S.dpre[k] = d; S.dpost[k] = d; S.rpre[k] = r; S.rpost[k] = r;
-    S.pdist[k] = P.s.pdist[o];
-    S.gmt[k] = P.s.gmt[o];
-    S.sfilt[k] = P.s.sfilt[o];
-    S.decon[k] = P.s.decon[o];
-    S.minrel[k] = P.s.minrel[o];
-    S.adiff[k] = P.s.adiff[o];
-  }
-  for (int k = lane; k < NCUR; k += WAVE) S.cur[k] = P.s.cur[(size_t)env * NCUR + k];
+  // ---- 0. the env's record HBM -> LDS (one round trip) + this step's actions ------------
   int ai = 0;
   if (P.mode == 0 && lane < N) {
     const size_t base = (size_t)env * N + lane;
@@ -1177,14 +1191,20 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams P) {
       for (int q = 1; q < 25; ++q) if (a[q] > best) { best = a[q]; ai = q; }
     }
   }
-  const int cstep = P.s.step[env] + 1;
+  rec_copy<LPE>(P.s.rec + (size_t)env * P.s.rec_stride16, (float4*)lbase, P.s.rec16);
+  __syncthreads();
+  if (lane < N) {
+    S.dpre[lane] = S.dpost[lane];
+    S.rpre[lane] = S.rpost[lane];
+  }
+  const int cstep = S.step[0] + 1;
   __syncthreads();
   STAMP(1);
 
   if (P.mode == 1) {
-    reset_env<DYN>(P, S, env);
+    reset_env<DYN, LPE>(P, S, env);
     __syncthreads();
-    store_state<DYN>(P, S, env, true);
+    store_state<DYN, LPE>(P, S, lbase, env, true);
     return;
   }
 
@@ -1192,7 +1212,7 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams P) {
   if (P.emit_edges) {
     uint8_t* eo = P.o.edges + (size_t)env * E * E;
     const uint64_t m0 = ego_mask(S, N, P.L, N);
-    for (int u = lane; u < E * E; u += WAVE) {
+    for (int u = lane; u < E * E; u += LPE) {
       const int a = fdiv(u, P.m_E), b = u - a * E;
       double d = 0.0;
       if (a != b) {
@@ -1223,7 +1243,7 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams P) {
   const bool filter_on = S.cur[C_FILT] != 0.0;
   if (filter_on) {
     const int npairs = N * N;
-    for (int p = lane; p < npairs; p += WAVE) {
+    for (int p = lane; p < npairs; p += LPE) {
       const int i = p / N, j = p - i * N;
       if (i == j || S.dpre[i] || S.dpre[j]) continue;
       const double ex = S.ps[i], ey = S.ps[N + i], ox = S.ps[j], oy = S.ps[N + j];
@@ -1278,15 +1298,23 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams P) {
       const double th0 = s2, v0 = s3, w = a0, ac = a1;
       const double th1 = th0 + w * dt;
       const double v1 = v0 + ac * dt;
-      if (w == 0.0) {
-        const double dd = v0 * dt + 0.5 * ac * dt * dt;
-        x = x + dd * cos(th0);
-        y = y + dd * sin(th0);
+      // stable closed form about the mid-heading (oracle/lsm_oracle.py closed_form_step)
+      const double h = 0.5 * w * dt;
+      const double m = th0 + h;
+      const double cm = cos(m), sm = sin(m);
+      double sc, q;
+      if (fabs(h) < 0.1) {
+        const double h2 = h * h;
+        sc = 1.0 - h2 / 6.0 * (1.0 - h2 / 20.0 * (1.0 - h2 / 42.0 * (1.0 - h2 / 72.0)));
+        q = -h / 3.0 * (1.0 - h2 / 10.0 * (1.0 - h2 / 28.0 * (1.0 - h2 / 54.0)));
       } else {
-        const double sn1 = sin(th1), cs1 = cos(th1), sn0 = sin(th0), cs0 = cos(th0);
-        x = x + (v1 * sn1 - v0 * sn0) / w + ac * (cs1 - cs0) / (w * w);
-        y = y + (-v1 * cs1 + v0 * cs0) / w + ac * (sn1 - sn0) / (w * w);
+        sc = sin(h) / h;
+        q = (cos(h) - sc) / h;
       }
+      const double A = v0 * dt + 0.5 * ac * dt * dt;
+      const double B = 0.5 * ac * dt * dt;
+      x = x + (A * cm * sc + B * sm * q);
+      y = y + (A * sm * sc - B * cm * q);
       s2 = th1;
       s3 = v1;
       if (s3 > P.max_speed) s3 = P.max_speed;
@@ -1300,7 +1328,7 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams P) {
   STAMP(5);
 
   // ---- 5. distances, min relative distance ---------------------------------------------
-  compute_dist(P, S);
+  compute_dist<LPE>(P, S);
   if (lane < N) {
     const int i = lane;
     double m = INFINITY;
@@ -1317,7 +1345,7 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams P) {
 
   // ---- 6. obs, reward, goal/done update ---------------------------------------------------
   double mag = 0.0;
-  if (DYN == 0 && !P.use_filter_arg) mag = magnetic_penalty_wave(P, S, S.dpair);
+  if (DYN == 0 && !P.use_filter_arg) mag = magnetic_penalty_wave<LPE>(P, S, S.dpair);
   double rew = 0.0;
   double th_pre = 0.0, spd_pre = 0.0;
   bool reached_pre = false;
@@ -1480,26 +1508,33 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams P) {
     my_done = S.dpost[i] || cstep >= P.episode_length;
     P.o.dones[(size_t)env * N + i] = my_done ? 1 : 0;
   }
-  const bool all_done = __all(my_done);
+  bool all_done;
+  if (G == 1) {
+    all_done = __all(my_done);
+  } else {
+    const uint64_t gm = ((LPE == 64) ? ~0ull : ((1ull << LPE) - 1)) << (grp * LPE);
+    all_done = (__ballot(my_done) & gm) == gm;
+  }
   __syncthreads();
   STAMP(9);
 
   // ---- 9. graph outputs, or the auto-reset (whose outputs replace them) ---------------------
-  if (lane == 0) P.s.step[env] = cstep;
+  if (lane == 0) S.step[0] = cstep;
   if (P.auto_reset && all_done) {
     if (lane == 0) P.o.reset_flag[env] = 1;
-    reset_env<DYN>(P, S, env);
+    reset_env<DYN, LPE>(P, S, env);
     __syncthreads();
     STAMP(12);
-    store_state<DYN>(P, S, env, true);
+    store_state<DYN, LPE>(P, S, lbase, env, true);
   } else {
     if (lane == 0) P.o.reset_flag[env] = 0;
-    emit_graph<DYN>(P, S, env);
+    emit_graph<DYN, LPE>(P, S, env);
     __syncthreads();
     STAMP(10);
-    store_state<DYN>(P, S, env, false);
+    store_state<DYN, LPE>(P, S, lbase, env, false);
   }
   STAMP(11);
+  RTSTAMP(14);
 }
 
 // env k's MT19937: np.random.seed(seed + 1000 * (env_offset + k))
@@ -1532,6 +1567,7 @@ struct lsm_env {
   std::string err;
   bool tables_ok;
   int device;
+  int lpe;   // lanes per env: 64 (one env per wave), 32 or 16 (2 or 4 envs per wave)
 };
 
 static int fail(lsm_env* e, const std::string& msg) {
@@ -1670,24 +1706,22 @@ int lsm_create(const lsm_config* cfg, lsm_env** out) {
   e->N = N; e->L = L; e->NL = N * L; e->E = N * (1 + L);
   e->F = cfg->dynamics == LSM_DOUBLE_INTEGRATOR ? 10 : 11;
   e->OBS = cfg->dynamics == LSM_DOUBLE_INTEGRATOR ? 7 : 6;
+  // Lanes per env: 64 = one env per wave (default; measured fastest at 4096 envs, where
+  // 4 waves/SIMD hide LDS/HBM latency), 32/16 = 2/4 envs per wave sharing the per-agent
+  // instruction stream (needs N <= lanes). LSM_LPE overrides.
+  e->lpe = 64;
+  if (const char* v = getenv("LSM_LPE")) e->lpe = atoi(v);
+  if (!(e->lpe == 16 || e->lpe == 32 || e->lpe == 64) || e->lpe < N)
+    return fail(e, "LSM_LPE must be 16, 32 or 64 and >= num_agents");
   HIPCHK(e, hipGetDevice(&e->device));
   const size_t n = cfg->num_envs;
   int r = 0;
-  r |= dalloc(e, &e->s.st, n * 4 * N);
-  r |= dalloc(e, &e->s.pdist, n * N);
-  r |= dalloc(e, &e->s.done, n * N);
-  r |= dalloc(e, &e->s.reached, n * N);
-  r |= dalloc(e, &e->s.lm, n * 6 * e->NL);
-  r |= dalloc(e, &e->s.gmt, n * N);
-  r |= dalloc(e, &e->s.step, n);
-  r |= dalloc(e, &e->s.cur, n * NCUR);
-  r |= dalloc(e, &e->s.stats, n * NSTAT * N);
+  const LdsPlan lp = lds_plan(N, e->NL, e->E, e->F);
+  e->s.rec16 = (uint32_t)(lp.rec / 16);
+  e->s.hot16 = (uint32_t)(lp.hot / 16);
+  e->s.rec_stride16 = (uint32_t)(((lp.rec + 127) / 128) * 8);   // 128-B aligned records
+  r |= dalloc(e, &e->s.rec, n * e->s.rec_stride16);
   r |= dalloc(e, &e->s.prev, n * 8);
-  r |= dalloc(e, &e->s.winfo, n * NWINFO * N);
-  r |= dalloc(e, &e->s.sfilt, n * N);
-  r |= dalloc(e, &e->s.decon, n * N);
-  r |= dalloc(e, &e->s.minrel, n * N);
-  r |= dalloc(e, &e->s.adiff, n * N);
   r |= dalloc(e, &e->s.mt, n * MT_WORDS);
   r |= dalloc(e, &e->pairs, (size_t)e->E * (e->E - 1) / 2 + 1);
   if (r) return 1;
@@ -1698,33 +1732,30 @@ int lsm_create(const lsm_config* cfg, lsm_env** out) {
     pr.push_back(0);
     HIPCHK(e, hipMemcpy(e->pairs, pr.data(), pr.size() * 2, hipMemcpyHostToDevice));
   }
-  HIPCHK(e, hipMemset(e->s.st, 0, n * 4 * N * 8));
-  HIPCHK(e, hipMemset(e->s.pdist, 0, n * N * 8));
-  HIPCHK(e, hipMemset(e->s.done, 0, n * N));
-  HIPCHK(e, hipMemset(e->s.reached, 0, n * N * 4));
-  HIPCHK(e, hipMemset(e->s.lm, 0, n * 6 * e->NL * 8));
-  HIPCHK(e, hipMemset(e->s.step, 0, n * 4));
-  HIPCHK(e, hipMemset(e->s.cur, 0, n * NCUR * 8));
-  HIPCHK(e, hipMemset(e->s.sfilt, 0, n * N));
-  HIPCHK(e, hipMemset(e->s.adiff, 0, n * N * 8));
   {
-    // reference initial values: prev summary (environment.py:873-881), stats (init_episode_agent_info)
-    std::vector<double> prev(n * 8, 0.0), stats(n * NSTAT * N, 0.0), winfo(n * NWINFO * N, -1.0),
-        minrel(n * N, INFINITY), gmt(n * N, INFINITY);
-    std::vector<int32_t> decon(n * N, -1);
-    for (size_t k = 0; k < n; ++k) {
-      prev[k * 8 + 0] = cfg->episode_length;
-      for (int i = 0; i < N; ++i) {
-        stats[k * NSTAT * N + 4 * N + i] = INFINITY;
-        winfo[k * NWINFO * N + 3 * N + i] = 0.0;
-      }
+    // reference initial values: prev summary (environment.py:873-881), stats and info
+    // accumulators (init_episode_agent_info), decon -1, min distances inf
+    const size_t stride = (size_t)e->s.rec_stride16 * 16;
+    std::vector<unsigned char> rec(stride, 0);
+    double* stats = (double*)(rec.data() + lp.off[1]);
+    double* winfo = (double*)(rec.data() + lp.off[2]);
+    double* gmt = (double*)(rec.data() + lp.off[4]);
+    double* minrel = (double*)(rec.data() + lp.off[5]);
+    int32_t* decon = (int32_t*)(rec.data() + lp.off[10]);
+    for (int i = 0; i < N; ++i) {
+      stats[4 * N + i] = INFINITY;
+      for (int q = 0; q < 3; ++q) winfo[q * N + i] = -1.0;
+      winfo[3 * N + i] = 0.0;
+      gmt[i] = INFINITY;
+      minrel[i] = INFINITY;
+      decon[i] = -1;
     }
+    std::vector<unsigned char> all(n * stride);
+    for (size_t k = 0; k < n; ++k) memcpy(all.data() + k * stride, rec.data(), stride);
+    HIPCHK(e, hipMemcpy(e->s.rec, all.data(), all.size(), hipMemcpyHostToDevice));
+    std::vector<double> prev(n * 8, 0.0);
+    for (size_t k = 0; k < n; ++k) prev[k * 8 + 0] = cfg->episode_length;
     HIPCHK(e, hipMemcpy(e->s.prev, prev.data(), prev.size() * 8, hipMemcpyHostToDevice));
-    HIPCHK(e, hipMemcpy(e->s.stats, stats.data(), stats.size() * 8, hipMemcpyHostToDevice));
-    HIPCHK(e, hipMemcpy(e->s.winfo, winfo.data(), winfo.size() * 8, hipMemcpyHostToDevice));
-    HIPCHK(e, hipMemcpy(e->s.minrel, minrel.data(), minrel.size() * 8, hipMemcpyHostToDevice));
-    HIPCHK(e, hipMemcpy(e->s.gmt, gmt.data(), gmt.size() * 8, hipMemcpyHostToDevice));
-    HIPCHK(e, hipMemcpy(e->s.decon, decon.data(), decon.size() * 4, hipMemcpyHostToDevice));
   }
   hipLaunchKernelGGL(seed_kernel, dim3((n + 255) / 256), dim3(256), 0, 0, e->s.mt, (int)n, cfg->seed,
                      cfg->env_offset);
@@ -1827,13 +1858,27 @@ static int check_ready(lsm_env* e, bool stepping) {
   return 0;
 }
 
+extern "C++" template <int DYN, int LPE>
+static void launch_t(lsm_env* e, const KParams& P, size_t env_lds, hipStream_t st) {
+  constexpr int G = WAVE / LPE;
+  const int blocks = (e->cfg.num_envs + G - 1) / G;
+  hipLaunchKernelGGL((rollout_kernel<DYN, LPE>), dim3(blocks), dim3(WAVE), env_lds * G, st, P);
+}
+
 static int launch(lsm_env* e, KParams& P, hipStream_t st) {
-  const size_t lds = lds_plan(e->N, e->NL, e->E, e->F).bytes;
-  if (lds > 65536) return fail(e, "LDS footprint too large");
-  if (P.dyn == 0)
-    hipLaunchKernelGGL(rollout_kernel<0>, dim3(e->cfg.num_envs), dim3(WAVE), lds, st, P);
-  else
-    hipLaunchKernelGGL(rollout_kernel<1>, dim3(e->cfg.num_envs), dim3(WAVE), lds, st, P);
+  const size_t env_lds = lds_plan(e->N, e->NL, e->E, e->F).bytes;
+  if (env_lds * (WAVE / e->lpe) > 65536) return fail(e, "LDS footprint too large");
+  P.lds_env_bytes = (uint32_t)env_lds;
+  const int k = (P.dyn ? 4 : 0) + (e->lpe == 64 ? 0 : e->lpe == 32 ? 1 : e->lpe == 16 ? 2 : 3);
+  switch (k) {
+    case 0: launch_t<0, 64>(e, P, env_lds, st); break;
+    case 1: launch_t<0, 32>(e, P, env_lds, st); break;
+    case 2: launch_t<0, 16>(e, P, env_lds, st); break;
+    case 4: launch_t<1, 64>(e, P, env_lds, st); break;
+    case 5: launch_t<1, 32>(e, P, env_lds, st); break;
+    case 6: launch_t<1, 16>(e, P, env_lds, st); break;
+    default: return fail(e, "unsupported lanes-per-env");
+  }
   HIPCHK(e, hipGetLastError());
   return 0;
 }

@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--config", type=int, default=3)
     ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--build", action="store_true")
+    ap.add_argument("--envs", type=int, default=0)
     a = ap.parse_args()
     if a.build or not os.path.exists(STAMP_LIB):
         build_stamps()
@@ -48,21 +49,24 @@ def main():
     args = bench.make_args(c)
     vt, tt = hj_tables.default_tables(c["dynamics_type"]) if (c["use_safety_filter"] or
                                                               c["dynamics_type"] != "double_integrator") else (None, None)
-    env = GpuGraphVecEnv(args, num_envs=c["envs"], device="cuda:0", value_table=vt, ttr_table=tt,
+    n_envs = a.envs or c["envs"]
+    env = GpuGraphVecEnv(args, num_envs=n_envs, device="cuda:0", value_table=vt, ttr_table=tt,
                          return_numpy=False, build_infos=False)
-    stamps = torch.zeros((c["envs"], 16), dtype=torch.int64, device="cuda:0")
+    stamps = torch.zeros((n_envs, 16), dtype=torch.int64, device="cuda:0")
     capi.check(env.lib.lsm_bind_output(env.h, capi.OUT_DEBUG_STAMPS, C.c_void_p(stamps.data_ptr()),
                                        stamps.numel() * 8), env.h)
     env.reset(4)
     N = c["num_agents"]
-    acc = []
+    acc, rt = [], []
     for t in range(a.steps + 10):
-        act = torch.randint(0, 25, (c["envs"], N), device="cuda:0", dtype=torch.int32)
+        act = torch.randint(0, 25, (n_envs, N), device="cuda:0", dtype=torch.int32)
         env.step(act, 4)
         torch.cuda.synchronize()
         if t >= 10:
             s = stamps.cpu().numpy().astype(np.float64)
             acc.append(np.diff(s[:, [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10]], axis=1))
+            t0 = s[:, 13].min()
+            rt.append(np.stack([s[:, 13] - t0, s[:, 14] - t0], axis=1) * 10.0)   # ns (100 MHz)
     d = np.concatenate(acc, axis=0)
     med = np.median(d, axis=0)
     tot = med.sum()
@@ -70,6 +74,12 @@ def main():
     for name, v in zip(PHASES, med):
         print("%-18s %12.0f   %5.1f%%" % (name, v, 100 * v / tot))
     print("%-18s %12.0f" % ("total", tot))
+    r = np.stack(rt)   # [steps][envs][2] ns since the first wave started
+    q = lambda x: "p0 %.2f  p10 %.2f  p50 %.2f  p90 %.2f  p100 %.2f us" % tuple(
+        np.percentile(x, [0, 10, 50, 90, 100]) / 1e3)
+    print("wave start  ", q(r[..., 0].ravel()))
+    print("wave end    ", q(r[..., 1].ravel()))
+    print("wave life   ", q((r[..., 1] - r[..., 0]).ravel()))
     env.close()
 
 

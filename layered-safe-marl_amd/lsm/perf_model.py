@@ -3,11 +3,12 @@
 Counts the bytes that MUST cross HBM for one env-step of the reference-layout
 path, per env:
 
-* state read + written back: agent state 4N f64, travel distance N f64, done N u8,
-  reached_goal N i32, landmarks 4NL f64 (read; written back), step counter i32,
-  curriculum block 12 f64 (read), episode stats 6N f64, info accumulators 4N f64,
-  goal_min_time N f64 (read), safety flags / indices / min distance / action diff
-  (N u8 + N i32 + 2N f64, written);
+* the env's persistent record (lsm_rollout.hip StateDev / lds_plan), read whole and
+  written back up to the curriculum block: agent state 4N f64, episode stats 6N f64,
+  info accumulators 4N f64, travel distance / goal_min_time / min relative distance /
+  action diff N f64 each, done / reached / safety flag / deconflicting index N i32
+  each, step counter i32 (every field 16-B aligned) | curriculum block 12 f64 and
+  landmarks 6NL f64 (read only; written back only at a reset);
 * actions: N i32 read;
 * outputs written: obs N*OBS f32, node_obs N*E*F f32, adj N*E*E f32, reward N f32,
   done N u8, reset flag 1 u8, info N*16 f64, state copy 4N f64.
@@ -25,13 +26,15 @@ def step_bytes(N: int, L: int = 2, dynamics: str = "double_integrator", filter_o
     di = dynamics == "double_integrator"
     F = 10 if di else 11
     OBS = 7 if di else 6
-    state_rw = 2 * (4 * N * 8 + N * 8 + N + N * 4 + 4 * NL * 8 + 4 + 6 * N * 8 + 4 * N * 8)
-    state_r = 12 * 8 + N * 8 + N * 4
-    state_w = N + N * 4 + 2 * N * 8
+    a16 = lambda x: (x + 15) // 16 * 16
+    hot = (a16(8 * 4 * N) + a16(8 * 6 * N) + a16(8 * 4 * N) + 4 * a16(8 * N) + 4 * a16(4 * N) + 16)
+    rec = hot + a16(8 * 12) + a16(8 * 6 * NL)
+    state_r = rec + N * 4
+    state_w = hot
     outputs = N * OBS * 4 + N * E * F * 4 + N * E * E * 4 + N * 4 + N + 1 + N * 16 * 8 + 4 * N * 8
-    hbm = state_rw + state_r + state_w + outputs
+    hbm = state_r + state_w + outputs
     corners = 16 if di else 32
     gw = 16 if di else 32
     gathers = (corners * 4 * N * (N - 1) + corners * gw * N) if filter_on else 0
-    return dict(hbm_bytes=hbm, outputs=outputs, state=state_rw + state_r + state_w, gather_bytes=gathers,
+    return dict(hbm_bytes=hbm, outputs=outputs, state=state_r + state_w, gather_bytes=gathers,
                 E=E, F=F, OBS=OBS)

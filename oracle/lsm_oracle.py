@@ -877,14 +877,24 @@ def closed_form_step(y, a, dt, di):
     w, ac = a0, a1
     th1 = th0 + w * dt
     v1 = v0 + ac * dt
-    if w == 0.0:
-        dd = v0 * dt + 0.5 * ac * dt * dt
-        px = y[0] + dd * math.cos(th0)
-        py = y[1] + dd * math.sin(th0)
+    # Stable closed form around the mid-heading m = th0 + h, h = w dt / 2 (no 1/w, 1/w^2
+    # cancellation for a filtered |w| ~ 1e-9):
+    #   dx = A cos(m) sinc(h) + B sin(m) q(h),  dy = A sin(m) sinc(h) - B cos(m) q(h)
+    # with A = v0 dt + a dt^2 / 2, B = a dt^2 / 2, q(h) = (cos h - sinc h) / h.
+    h = 0.5 * w * dt
+    m = th0 + h
+    cm, sm = math.cos(m), math.sin(m)
+    if abs(h) < 0.1:
+        h2 = h * h
+        sc = 1.0 - h2 / 6.0 * (1.0 - h2 / 20.0 * (1.0 - h2 / 42.0 * (1.0 - h2 / 72.0)))
+        q = -h / 3.0 * (1.0 - h2 / 10.0 * (1.0 - h2 / 28.0 * (1.0 - h2 / 54.0)))
     else:
-        s1, c1, s0, c0 = math.sin(th1), math.cos(th1), math.sin(th0), math.cos(th0)
-        px = y[0] + (v1 * s1 - v0 * s0) / w + ac * (c1 - c0) / (w * w)
-        py = y[1] + (-v1 * c1 + v0 * c0) / w + ac * (s1 - s0) / (w * w)
+        sc = math.sin(h) / h
+        q = (math.cos(h) - sc) / h
+    A = v0 * dt + 0.5 * ac * dt * dt
+    B = 0.5 * ac * dt * dt
+    px = y[0] + (A * cm * sc + B * sm * q)
+    py = y[1] + (A * sm * sc - B * cm * q)
     return np.array([px, py, th1, v1])
 
 

@@ -107,14 +107,17 @@ CASES = [
 ]
 
 
+@pytest.mark.parametrize("lpe", [16, 32, 64])
 @pytest.mark.parametrize("case", range(len(CASES)))
-def test_gpu_matches_oracle_multi_env(case):
-    """16 envs with per-env seeds seed + 1000 k, random actions, across an auto-reset."""
+def test_gpu_matches_oracle_multi_env(case, lpe, monkeypatch):
+    """16 (or 15: a partly filled last wave) envs with per-env seeds seed + 1000 k, random
+    actions, across an auto-reset; every lanes-per-env kernel variant (1, 2 or 4 envs/wave)."""
+    monkeypatch.setenv("LSM_LPE", str(lpe))
     c = dict(CASES[case])
     ep = c.pop("ep")
     meta = dict(num_landmarks=2, n_rollout_threads=1, use_masking=True, num_internal_step=1, seed=5,
                 env_seed=5, **c)
-    n_envs, steps = 16, min(c["episode_length"] + 20, 120)
+    n_envs, steps = (16 if lpe == 64 else 15), min(c["episode_length"] + 20, 120)
     env = _gpu_env(meta, n_envs=n_envs, seed=5)
     ora = _oracle_for(meta, 5, n_envs)
     g = env.reset(ep)

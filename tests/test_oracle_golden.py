@@ -101,6 +101,19 @@ def test_closed_form_airtaxi_accuracy():
         np.testing.assert_allclose(closed_form_step(s, a, 1.0, False), ref, rtol=0, atol=1e-11)
 
 
+def test_closed_form_airtaxi_tiny_turn_rate():
+    """A filtered turn rate can be ~1e-9 (QP projection): the closed form must not divide
+    by w / w^2 there (the naive form loses ~1e-4 to cancellation)."""
+    from scipy.integrate import solve_ivp
+    rng = np.random.default_rng(2)
+    for w in [0.0, 1e-15, -3e-12, 1e-9, -2e-7, 1e-5, 0.05, 0.1999, 0.2001, -0.3]:
+        s = np.array([rng.uniform(-3, 3), rng.uniform(-3, 3), rng.uniform(-4, 4), rng.uniform(0.03, 0.09)])
+        a = np.array([w, rng.uniform(-0.001, 0.002)])
+        ode = lambda t, y: np.array([y[3] * np.cos(y[2]), y[3] * np.sin(y[2]), a[0], a[1]])
+        ref = solve_ivp(ode, [0, 1.0], s, method="DOP853", rtol=1e-13, atol=1e-15).y[:, -1]
+        np.testing.assert_allclose(closed_form_step(s, a, 1.0, False), ref, rtol=0, atol=1e-13)
+
+
 def test_grid_semantics_periodic_and_domain():
     g = Grid([-1.0, -np.pi], [1.0, np.pi], (5, 8), periodic_dims=(1,))
     vals = np.arange(40, dtype=np.float32).reshape(5, 8)
