@@ -149,33 +149,32 @@ def main():
     env.reset(ep)
     epl = c["episode_length"]
 
-    def one_step(t, ev=None):
-        acts = acts_all[t]
-        if ev is not None:
-            ev[0].record()
-        env.step_async(acts, ep)
-        if ev is not None:
-            ev[1].record()
+    def one_step(t):
+        env.step_async(acts_all[t], ep)
         env.step_wait()
         if (t + 1) % epl == 0:   # episode boundary: RCCL reduction of the episode summary
             global_episode_summary(env.t_epinfo)
 
     for t in range(a.warmup):
         one_step(t)
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+    # Kernel time: HIP events on the launch stream bracketing the whole timed region (per-launch
+    # event pairs would add their own GPU-side markers between back-to-back launches).
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    ev0.record()
     for t in range(a.steps):
-        one_step(a.warmup + t, evs[t])
+        one_step(a.warmup + t)
+    ev1.record()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    kern_ms = sum(e0.elapsed_time(e1) for e0, e1 in evs) / a.steps
+    kern_ms = ev0.elapsed_time(ev1) / a.steps   # includes the inter-launch gaps (conservative)
     if world > 1:
         tt_ = torch.tensor([elapsed, kern_ms], device=dev, dtype=torch.float64)
         dist.all_reduce(tt_, op=dist.ReduceOp.MAX)

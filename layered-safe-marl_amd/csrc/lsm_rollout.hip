@@ -42,8 +42,10 @@
   do {                                                                                       \
     __syncthreads();                                                                         \
     if (lane == 0 && P.stamps) P.stamps[(size_t)env * 16 + (k)] = __builtin_amdgcn_s_memtime(); \
+    if (L.stop_after == (k)) return;  /* per-phase instruction counting (lsm.diag_stamps) */ \
   } while (0)
-// slots 13/14: 100 MHz chip-wide clock at wave start / end (dispatch ramp and tail)
+// slots 13/14: 100 MHz chip-wide clock at wave start / end (dispatch ramp and tail);
+// slot 15: HW_ID (wave, simd, cu, se) | XCC_ID << 32
 #define RTSTAMP(k)                                                                           \
   do {                                                                                       \
     if (lane == 0 && P.stamps) P.stamps[(size_t)env * 16 + (k)] = __builtin_amdgcn_s_memrealtime(); \
@@ -114,8 +116,7 @@ struct OutDev {
 };
 
 struct KParams {
-  int n_envs, N, L, NL, E, F, OBS, dyn, episode_length, use_masking, use_filter_arg, auto_reset,
-      emit_edges, action_kind, mode;  // mode 0 = step, 1 = reset all
+  int n_envs, N, L, NL, E, F, OBS, dyn, episode_length, use_masking, use_filter_arg, auto_reset;
   double dt, world_size, coord_range, world_eng, sep_target, max_speed, min_speed, gs_min, gs_max;
   double act0[5], act1[5];
   double mag_c[50], mag_s[50];
@@ -124,15 +125,20 @@ struct KParams {
   double at_vmax, at_vmin, at_amax, at_amin, at_wmax, at_thr_amax, at_thr_amin;
   float at_box_w, at_box_amax, at_box_amin;  // float32 box corners (jnp)
   double ttr_max;
-  double cur_new[NCUR];
-  uint32_t m_E, m_EE, m_EF, m_F;  // ceil(2^32 / d) for exact small-numerator division
+  uint32_t m_E, m_EE, m_EF, m_F, m_EF4;  // ceil(2^32 / d) for exact small-numerator division
   unsigned long long* stamps;     // LSM_OUT_DEBUG_STAMPS (diagnostic builds only)
   uint32_t lds_env_bytes;         // LDS bytes per env (envs per wave > 1: consecutive blocks)
   const uint16_t* pairs;          // strict upper-triangle entity pairs (a | b << 8)
   TableDev val, ttr;
   StateDev s;
   OutDev o;
+};
+
+// Per-launch kernel arguments (the rest lives in a device-resident KParams per handle).
+struct KStep {
   const void* actions;
+  int action_kind, mode, emit_edges, stop_after;   // mode 0 = step, 1 = reset all
+  double cur_new[NCUR];
 };
 
 // ----------------------------------------------------------------------------------
@@ -191,6 +197,16 @@ struct LdsPlan {
 
 // q / d for q * d < 2^32 (all index math here): __umulhi(q, ceil(2^32 / d))
 __device__ __forceinline__ int fdiv(int q, uint32_t m) { return (int)__umulhi((uint32_t)q, m); }
+
+// all() over the LPE-lane group of the calling lane (one env)
+template <int LPE>
+__device__ __forceinline__ bool group_all(bool v) {
+  if (LPE == 64) return __all(v);
+  const uint64_t b = __ballot(v);
+  const int g = (int)threadIdx.x / LPE;
+  const uint64_t gm = ((1ull << LPE) - 1) << (g * LPE);
+  return (b & gm) == gm;
+}
 
 __host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
 
@@ -911,27 +927,70 @@ __device__ __forceinline__ void emit_graph(const KParams& P, Lds& S, int env) {
   const int N = P.N, E = P.E, F = P.F;
   if (DYN == 0) build_rows_di<LPE>(P, S);
   __syncthreads();
+  // No agent changed done / reached status this step (the common case): every ego then has
+  // the same disconnect mask and the same (pre == post) entity rows, so each lane computes
+  // its output words once and stores them for all N egos.
+  const bool uni = group_all<LPE>(lane >= N || (S.dpre[lane] == S.dpost[lane] && S.rpre[lane] == S.rpost[lane]));
   // ---- adjacency: ego e, row r, col c ------------------------------------------------------
   const int EE = E * E, atot = N * EE;
   float* adj_out = P.o.adj + (size_t)env * atot;
-  if ((E & 3) == 0) {
-    for (int q0 = lane * 4; q0 < atot; q0 += LPE * 4) {
-      const int e = fdiv(q0, P.m_EE);
-      const int u = q0 - e * EE;
-      const int r = fdiv(u, P.m_E);
-      const int c = u - r * E;
-      const uint64_t m = S.emask[e];
-      float4 v = *(const float4*)(S.fval + u);
-      if ((m >> r) & 1ull) {
-        v = make_float4(0.f, 0.f, 0.f, 0.f);
-      } else {
-        const uint32_t bits = (uint32_t)(m >> c) & 0xfu;
-        if (bits & 1u) v.x = 0.f;
-        if (bits & 2u) v.y = 0.f;
-        if (bits & 4u) v.z = 0.f;
-        if (bits & 8u) v.w = 0.f;
+  if ((E & 3) == 0 && uni) {
+    const int Q = EE / 4, last = Q - 1;
+    const uint64_t m = S.emask[0];
+    for (int t0 = lane; t0 < Q; t0 += 4 * LPE) {
+      int u[4];
+      float4 w[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int t = t0 + j * LPE;
+        u[j] = 4 * (t < last ? t : last);
+        const int r = fdiv(u[j], P.m_E);
+        const int c = u[j] - r * E;
+        w[j] = *(const float4*)(S.fval + u[j]);
+        const uint32_t bits = ((m >> r) & 1ull) ? 0xfu : ((uint32_t)(m >> c) & 0xfu);
+        if (bits & 1u) w[j].x = 0.f;
+        if (bits & 2u) w[j].y = 0.f;
+        if (bits & 4u) w[j].z = 0.f;
+        if (bits & 8u) w[j].w = 0.f;
       }
-      *(float4*)(adj_out + q0) = v;
+      for (int e = 0; e < N; ++e) {
+        float* dst = adj_out + (size_t)e * EE;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (t0 + j * LPE <= last) *(float4*)(dst + u[j]) = w[j];
+      }
+    }
+  } else if ((E & 3) == 0) {
+    // Each lane owns fixed float4 column groups u of the E x E table (loaded from LDS once)
+    // and writes them for every ego: per ego only the mask word is read.
+    const int Q = EE / 4;
+    for (int t0 = lane; t0 < Q; t0 += 4 * LPE) {
+      const int last = Q - 1;
+      int u[4], rr[4];
+      float4 v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int t = t0 + j * LPE;
+        u[j] = 4 * (t < last ? t : last);
+        rr[j] = fdiv(u[j], P.m_E);
+        v[j] = *(const float4*)(S.fval + u[j]);
+      }
+      for (int e = 0; e < N; ++e) {
+        const uint64_t m = S.emask[e];
+        float* dst = adj_out + (size_t)e * EE;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if (t0 + j * LPE > last) break;
+          float4 w = v[j];
+          const int c = u[j] - rr[j] * E;
+          const uint32_t bits = ((m >> rr[j]) & 1ull) ? 0xfu : ((uint32_t)(m >> c) & 0xfu);
+          if (bits & 1u) w.x = 0.f;
+          if (bits & 2u) w.y = 0.f;
+          if (bits & 4u) w.z = 0.f;
+          if (bits & 8u) w.w = 0.f;
+          *(float4*)(dst + u[j]) = w;
+        }
+      }
     }
   } else {
     for (int q = lane; q < atot; q += LPE) {
@@ -943,10 +1002,54 @@ __device__ __forceinline__ void emit_graph(const KParams& P, Lds& S, int env) {
       adj_out[q] = (((m >> r) | (m >> c)) & 1ull) ? 0.0f : S.fval[u];
     }
   }
-  __syncthreads();   // fval dead from here: node staging reuses U1
   // ---- node features --------------------------------------------------------------
   const int npairs = N * E, ntot = npairs * F;
   float* node_out = P.o.node + (size_t)env * ntot;
+  if (DYN == 0 && ((E * F) & 3) == 0 && uni) {
+    // lane owns float4 t of every ego block: entity rows read once, ego offset per ego
+    const int EF4 = E * F / 4;
+    for (int t = lane; t < EF4; t += LPE) {
+      int k = fdiv(4 * t, P.m_F);
+      int q = 4 * t - k * F;
+      double fv[4];
+      int qq[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        fv[c] = S.feat[(N + k) * F + q];   // post rows == pre rows here; landmarks at N + k
+        qq[c] = q;
+        if (++q == F) { q = 0; ++k; }
+      }
+      for (int e = 0; e < N; ++e) {
+        const double* o = S.egooff + e * F;
+        *(float4*)(node_out + (size_t)e * E * F + 4 * t) =
+            make_float4((float)(fv[0] - o[qq[0]]), (float)(fv[1] - o[qq[1]]), (float)(fv[2] - o[qq[2]]),
+                        (float)(fv[3] - o[qq[3]]));
+      }
+    }
+    return;
+  }
+  if (DYN == 0 && ((E * F) & 3) == 0) {
+    // DI: node[e][k][q] = f32(row(e, k)[q] - off(e)[q]); written straight from the rows as
+    // contiguous float4 (each ego block is E*F floats, a multiple of 4).
+    const int q4 = ntot / 4, EF4 = E * F / 4;
+    for (int t = lane; t < q4; t += LPE) {
+      const int e = fdiv(t, P.m_EF4);
+      const int j0 = 4 * (t - e * EF4);
+      int k = fdiv(j0, P.m_F);
+      int q = j0 - k * F;
+      const double* o = S.egooff + e * F;
+      float f[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int row = (k < N) ? ((k > e) ? k : N + k) : N + k;
+        f[c] = (float)(S.feat[row * F + q] - o[q]);
+        if (++q == F) { q = 0; ++k; }
+      }
+      *(float4*)(node_out + 4 * (size_t)t) = make_float4(f[0], f[1], f[2], f[3]);
+    }
+    return;
+  }
+  __syncthreads();   // fval dead from here: node staging reuses U1
   const bool nvec = (ntot & 3) == 0;
   for (int b0 = 0; b0 < npairs; b0 += LPE) {
     const int p = b0 + lane;
@@ -1074,7 +1177,7 @@ __device__ __forceinline__ void summary(const KParams& P, const Lds& S, double* 
 // Device reset of one env (MultiAgentGraphEnv.reset, environment.py:1046-1074). Expects the
 // env's persistent per-agent arrays in LDS (S.stats, S.rpost = reached_goal before reset).
 template <int DYN, int LPE>
-__device__ __forceinline__ void reset_env(const KParams& P, Lds& S, int env) {
+__device__ __forceinline__ void reset_env(const KParams& P, Lds& S, int env, const double* cur_new) {
   const int lane = threadIdx.x & (LPE - 1);
   const int N = P.N, NL = P.NL;
   double* prev = P.s.prev + (size_t)env * 8;
@@ -1087,7 +1190,7 @@ __device__ __forceinline__ void reset_env(const KParams& P, Lds& S, int env) {
     }
   }
   __syncthreads();
-  for (int k = lane; k < NCUR; k += LPE) S.cur[k] = P.cur_new[k];
+  for (int k = lane; k < NCUR; k += LPE) S.cur[k] = cur_new[k];
   const uint32_t* mtg = P.s.mt + (size_t)env * MT_WORDS;
   for (int k = lane; k < MT_WORDS; k += LPE) S.mt[k] = mtg[k];
   __syncthreads();
@@ -1162,7 +1265,8 @@ __device__ __forceinline__ void store_state(const KParams& P, Lds& S, const unsi
 }
 
 template <int DYN, int LPE>
-__global__ __launch_bounds__(64) void rollout_kernel(const KParams P) {
+__global__ __launch_bounds__(64) void rollout_kernel(const KParams* __restrict__ Pp, const KStep L) {
+  const KParams& P = *Pp;   // per-handle constants in device memory; per-launch fields in L
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int G = WAVE / LPE;   // envs per wave, one per LPE-lane group
   const int grp = (G == 1) ? 0 : (int)threadIdx.x / LPE;
@@ -1173,20 +1277,25 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams P) {
   unsigned char* lbase = smem + (size_t)grp * P.lds_env_bytes;
   Lds S = carve(lbase, N, NL, E, P.F);
   RTSTAMP(13);
+#ifdef LSM_STAMPS
+  if (lane == 0 && P.stamps)
+    P.stamps[(size_t)env * 16 + 15] = (unsigned long long)__builtin_amdgcn_s_getreg(63492) |
+                                      ((unsigned long long)__builtin_amdgcn_s_getreg(6164) << 32);
+#endif
   STAMP(0);
 
   // ---- 0. the env's record HBM -> LDS (one round trip) + this step's actions ------------
   int ai = 0;
-  if (P.mode == 0 && lane < N) {
+  if (L.mode == 0 && lane < N) {
     const size_t base = (size_t)env * N + lane;
-    if (P.action_kind == LSM_ACTIONS_INDEX_I32) {
-      ai = ((const int32_t*)P.actions)[base];
-    } else if (P.action_kind == LSM_ACTIONS_ONEHOT_F32) {
-      const float* a = (const float*)P.actions + base * 25;
+    if (L.action_kind == LSM_ACTIONS_INDEX_I32) {
+      ai = ((const int32_t*)L.actions)[base];
+    } else if (L.action_kind == LSM_ACTIONS_ONEHOT_F32) {
+      const float* a = (const float*)L.actions + base * 25;
       float best = a[0];
       for (int q = 1; q < 25; ++q) if (a[q] > best) { best = a[q]; ai = q; }
     } else {
-      const double* a = (const double*)P.actions + base * 25;
+      const double* a = (const double*)L.actions + base * 25;
       double best = a[0];
       for (int q = 1; q < 25; ++q) if (a[q] > best) { best = a[q]; ai = q; }
     }
@@ -1201,15 +1310,15 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams P) {
   __syncthreads();
   STAMP(1);
 
-  if (P.mode == 1) {
-    reset_env<DYN, LPE>(P, S, env);
+  if (L.mode == 1) {
+    reset_env<DYN, LPE>(P, S, env, L.cur_new);
     __syncthreads();
     store_state<DYN, LPE>(P, S, lbase, env, true);
     return;
   }
 
   // ---- 1. update_graph() at step start (previous state, final masks) --------------
-  if (P.emit_edges) {
+  if (L.emit_edges) {
     uint8_t* eo = P.o.edges + (size_t)env * E * E;
     const uint64_t m0 = ego_mask(S, N, P.L, N);
     for (int u = lane; u < E * E; u += LPE) {
@@ -1457,7 +1566,7 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams P) {
     double dm, ds, tm, ts;
     np_mean_std(Snap{S.wnew, S.wold, i}, N, dm, ds);
     np_mean_std(Snap{S.wnew + N, S.wold + N, i}, N, tm, ts);
-    double* inf = P.o.info + ((size_t)env * N + i) * LSM_INFO_FIELDS;
+    double* inf = S.dpair + i * LSM_INFO_FIELDS;   // staged in U2 (filter scratch is dead)
     const double mr = S.minrel[i];
     inf[LSM_INFO_INDIVIDUAL_REWARD] = rew;
     inf[LSM_INFO_MIN_RELATIVE_DISTANCE] = mr;
@@ -1476,6 +1585,9 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams P) {
     inf[LSM_INFO_ACTION_DIFF] = S.adiff[i];
     inf[LSM_INFO_REACHED_GOAL] = (double)S.rpost[i];
   }
+  __syncthreads();
+  rec_copy<LPE>((const float4*)S.dpair, (float4*)(P.o.info + (size_t)env * N * LSM_INFO_FIELDS),
+                N * LSM_INFO_FIELDS / 2);
   STAMP(8);
 
   // ---- episode stats (environment.py:1004-1022), dones ---------------------------------
@@ -1508,13 +1620,7 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams P) {
     my_done = S.dpost[i] || cstep >= P.episode_length;
     P.o.dones[(size_t)env * N + i] = my_done ? 1 : 0;
   }
-  bool all_done;
-  if (G == 1) {
-    all_done = __all(my_done);
-  } else {
-    const uint64_t gm = ((LPE == 64) ? ~0ull : ((1ull << LPE) - 1)) << (grp * LPE);
-    all_done = (__ballot(my_done) & gm) == gm;
-  }
+  const bool all_done = group_all<LPE>(my_done);
   __syncthreads();
   STAMP(9);
 
@@ -1522,7 +1628,7 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams P) {
   if (lane == 0) S.step[0] = cstep;
   if (P.auto_reset && all_done) {
     if (lane == 0) P.o.reset_flag[env] = 1;
-    reset_env<DYN, LPE>(P, S, env);
+    reset_env<DYN, LPE>(P, S, env, L.cur_new);
     __syncthreads();
     STAMP(12);
     store_state<DYN, LPE>(P, S, lbase, env, true);
@@ -1567,6 +1673,8 @@ struct lsm_env {
   std::string err;
   bool tables_ok;
   int device;
+  KParams* dparams;   // device copy of the per-handle constants (re-uploaded when dirty)
+  bool params_dirty;
   int lpe;   // lanes per env: 64 (one env per wave), 32 or 16 (2 or 4 envs per wave)
 };
 
@@ -1601,7 +1709,6 @@ static void fill_params(const lsm_env* e, KParams& P) {
   P.use_masking = e->cfg.use_masking;
   P.use_filter_arg = e->cfg.use_safety_filter;
   P.auto_reset = e->cfg.auto_reset;
-  P.emit_edges = e->cfg.emit_edges && e->out_ptr[LSM_OUT_EDGES] != nullptr;
   P.world_size = e->cfg.world_size;
   const double pi = 3.141592653589793;
   P.pi = pi;
@@ -1640,6 +1747,7 @@ static void fill_params(const lsm_env* e, KParams& P) {
   P.m_EE = magic(e->E * e->E);
   P.m_EF = magic(e->E * e->F);
   P.m_F = magic(e->F);
+  P.m_EF4 = magic(e->E * e->F / 4);
   P.ttr_max = e->ttr_max;
   P.val = e->val;
   P.ttr = e->ttr;
@@ -1690,6 +1798,8 @@ int lsm_create(const lsm_config* cfg, lsm_env** out) {
   *out = e;
   e->cfg = *cfg;
   e->tables_ok = false;
+  e->dparams = nullptr;
+  e->params_dirty = true;
   e->ttr_max = 0.0;
   memset(&e->val, 0, sizeof(e->val));
   memset(&e->ttr, 0, sizeof(e->ttr));
@@ -1722,13 +1832,20 @@ int lsm_create(const lsm_config* cfg, lsm_env** out) {
   e->s.rec_stride16 = (uint32_t)(((lp.rec + 127) / 128) * 8);   // 128-B aligned records
   r |= dalloc(e, &e->s.rec, n * e->s.rec_stride16);
   r |= dalloc(e, &e->s.prev, n * 8);
+  r |= dalloc(e, &e->dparams, 1);
   r |= dalloc(e, &e->s.mt, n * MT_WORDS);
   r |= dalloc(e, &e->pairs, (size_t)e->E * (e->E - 1) / 2 + 1);
   if (r) return 1;
   {
+    // agent-agent pairs first (the only ones needing the float64 blocks), then
+    // agent-landmark, then landmark-landmark: the agent block stays in the first lane pass
     std::vector<uint16_t> pr;
-    for (int a = 0; a < e->E; ++a)
-      for (int b = a + 1; b < e->E; ++b) pr.push_back((uint16_t)(a | (b << 8)));
+    for (int cls = 0; cls < 3; ++cls)
+      for (int a = 0; a < e->E; ++a)
+        for (int b = a + 1; b < e->E; ++b) {
+          const int c = (a < N ? 0 : 1) + (b < N ? 0 : 1);
+          if (c == cls) pr.push_back((uint16_t)(a | (b << 8)));
+        }
     pr.push_back(0);
     HIPCHK(e, hipMemcpy(e->pairs, pr.data(), pr.size() * 2, hipMemcpyHostToDevice));
   }
@@ -1827,6 +1944,7 @@ int lsm_set_value_table(lsm_env* e, int32_t ndim, const double* lo, const double
   if (!grads) return fail(e, "value table needs its gradient table");
   if (upload_table(e, e->val, ndim, lo, hi, shape, periodic, values, grads)) return 1;
   e->tables_ok = (e->cfg.dynamics == LSM_DOUBLE_INTEGRATOR) || e->ttr.cells != nullptr;
+  e->params_dirty = true;
   return 0;
 }
 
@@ -1836,6 +1954,7 @@ int lsm_set_ttr_table(lsm_env* e, int32_t ndim, const double* lo, const double* 
   if (upload_table(e, e->ttr, ndim, lo, hi, shape, periodic, values, nullptr)) return 1;
   e->ttr_max = ttr_max;
   e->tables_ok = !e->cfg.use_safety_filter || e->val.cells != nullptr;
+  e->params_dirty = true;
   return 0;
 }
 
@@ -1844,6 +1963,7 @@ int lsm_bind_output(lsm_env* e, int32_t slot, void* ptr, size_t bytes) {
   const size_t need = lsm_output_bytes(e, slot);
   if (ptr && bytes < need) return fail(e, "output buffer too small for slot " + std::to_string(slot));
   e->out_ptr[slot] = ptr;
+  e->params_dirty = true;
   e->out_bytes[slot] = bytes;
   return 0;
 }
@@ -1859,24 +1979,36 @@ static int check_ready(lsm_env* e, bool stepping) {
 }
 
 extern "C++" template <int DYN, int LPE>
-static void launch_t(lsm_env* e, const KParams& P, size_t env_lds, hipStream_t st) {
+static void launch_t(lsm_env* e, const KStep& L, size_t env_lds, hipStream_t st) {
   constexpr int G = WAVE / LPE;
   const int blocks = (e->cfg.num_envs + G - 1) / G;
-  hipLaunchKernelGGL((rollout_kernel<DYN, LPE>), dim3(blocks), dim3(WAVE), env_lds * G, st, P);
+  hipLaunchKernelGGL((rollout_kernel<DYN, LPE>), dim3(blocks), dim3(WAVE), env_lds * G, st,
+                     (const KParams*)e->dparams, L);
 }
 
-static int launch(lsm_env* e, KParams& P, hipStream_t st) {
+static int launch(lsm_env* e, KStep& L, hipStream_t st) {
   const size_t env_lds = lds_plan(e->N, e->NL, e->E, e->F).bytes;
   if (env_lds * (WAVE / e->lpe) > 65536) return fail(e, "LDS footprint too large");
-  P.lds_env_bytes = (uint32_t)env_lds;
-  const int k = (P.dyn ? 4 : 0) + (e->lpe == 64 ? 0 : e->lpe == 32 ? 1 : e->lpe == 16 ? 2 : 3);
+  if (e->params_dirty) {   // outputs / tables changed: refresh the device copy (stream-ordered)
+    KParams P;
+    fill_params(e, P);
+    P.lds_env_bytes = (uint32_t)env_lds;
+    HIPCHK(e, hipMemcpyAsync(e->dparams, &P, sizeof(P), hipMemcpyHostToDevice, st));
+    HIPCHK(e, hipStreamSynchronize(st));
+    e->params_dirty = false;
+  }
+  L.stop_after = -1;
+#ifdef LSM_STAMPS
+  if (const char* v = getenv("LSM_STOP_AFTER")) L.stop_after = atoi(v);
+#endif
+  const int k = (e->cfg.dynamics ? 4 : 0) + (e->lpe == 64 ? 0 : e->lpe == 32 ? 1 : e->lpe == 16 ? 2 : 3);
   switch (k) {
-    case 0: launch_t<0, 64>(e, P, env_lds, st); break;
-    case 1: launch_t<0, 32>(e, P, env_lds, st); break;
-    case 2: launch_t<0, 16>(e, P, env_lds, st); break;
-    case 4: launch_t<1, 64>(e, P, env_lds, st); break;
-    case 5: launch_t<1, 32>(e, P, env_lds, st); break;
-    case 6: launch_t<1, 16>(e, P, env_lds, st); break;
+    case 0: launch_t<0, 64>(e, L, env_lds, st); break;
+    case 1: launch_t<0, 32>(e, L, env_lds, st); break;
+    case 2: launch_t<0, 16>(e, L, env_lds, st); break;
+    case 4: launch_t<1, 64>(e, L, env_lds, st); break;
+    case 5: launch_t<1, 32>(e, L, env_lds, st); break;
+    case 6: launch_t<1, 16>(e, L, env_lds, st); break;
     default: return fail(e, "unsupported lanes-per-env");
   }
   HIPCHK(e, hipGetLastError());
@@ -1886,25 +2018,25 @@ static int launch(lsm_env* e, KParams& P, hipStream_t st) {
 int lsm_reset(lsm_env* e, const lsm_curriculum* cur, void* stream) {
   if (!e || !cur) return 1;
   if (check_ready(e, false)) return 1;
-  KParams P;
-  fill_params(e, P);
-  memcpy(P.cur_new, cur, sizeof(double) * NCUR);
-  P.mode = 1;
-  P.emit_edges = 0;
-  return launch(e, P, (hipStream_t)stream);
+  KStep L;
+  memset(&L, 0, sizeof(L));
+  memcpy(L.cur_new, cur, sizeof(double) * NCUR);
+  L.mode = 1;
+  L.emit_edges = 0;
+  return launch(e, L, (hipStream_t)stream);
 }
 
 int lsm_step(lsm_env* e, const void* actions, int32_t kind, const lsm_curriculum* cur, void* stream) {
   if (!e || !actions || !cur) return fail(e, "null argument");
   if (kind < 0 || kind > 2) return fail(e, "bad action kind");
   if (check_ready(e, true)) return 1;
-  KParams P;
-  fill_params(e, P);
-  memcpy(P.cur_new, cur, sizeof(double) * NCUR);
-  P.mode = 0;
-  P.action_kind = kind;
-  P.actions = actions;
-  return launch(e, P, (hipStream_t)stream);
+  KStep L;
+  memcpy(L.cur_new, cur, sizeof(double) * NCUR);
+  L.mode = 0;
+  L.action_kind = kind;
+  L.actions = actions;
+  L.emit_edges = e->cfg.emit_edges && e->out_ptr[LSM_OUT_EDGES] != nullptr;
+  return launch(e, L, (hipStream_t)stream);
 }
 
 int lsm_host_mt_uniforms(uint32_t seed, int32_t count, double lo, double hi, double* out) {

@@ -80,6 +80,24 @@ def main():
     print("wave start  ", q(r[..., 0].ravel()))
     print("wave end    ", q(r[..., 1].ravel()))
     print("wave life   ", q((r[..., 1] - r[..., 0]).ravel()))
+    hw = stamps.cpu().numpy()[:, 15].astype(np.uint64)
+    xcc = (hw >> np.uint64(32)) & np.uint64(0xf)
+    hid = hw & np.uint64(0xffffffff)
+    simd = (hid >> np.uint64(4)) & np.uint64(3)
+    cu = (hid >> np.uint64(8)) & np.uint64(0xf)
+    se = (hid >> np.uint64(13)) & np.uint64(0x7)
+    life = (r[..., 1] - r[..., 0]).mean(axis=0) / 1e3   # per env, mean over steps (us)
+    print("mean wave life by XCC: " + " ".join("%d:%.1f" % (x, life[xcc == x].mean())
+                                                  for x in np.unique(xcc)))
+    print("mean wave life by SE:  " + " ".join("%d:%.1f" % (x, life[se == x].mean()) for x in np.unique(se)))
+    key = (xcc * np.uint64(1000) + se * np.uint64(100) + cu * np.uint64(4) + simd)
+    u, inv, cnt = np.unique(key, return_inverse=True, return_counts=True)
+    print("waves per SIMD (last step): min %d max %d  distinct SIMDs %d" % (cnt.min(), cnt.max(), len(u)))
+    per = np.array([life[inv == k].mean() for k in range(len(u))])
+    print("SIMD mean-life spread: p0 %.1f p50 %.1f p100 %.1f us" % tuple(np.percentile(per, [0, 50, 100])))
+    wv = [life[inv == k] for k in range(len(u))]
+    c = np.corrcoef(cnt[inv], life)[0, 1] if cnt.min() != cnt.max() else float("nan")
+    print("corr(waves on SIMD, life) %.2f" % c)
     env.close()
 
 
