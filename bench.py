@@ -155,6 +155,7 @@ def main():
         if (t + 1) % epl == 0:   # episode boundary: RCCL reduction of the episode summary
             global_episode_summary(env.t_epinfo)
 
+    global_episode_summary(env.t_epinfo)   # load the reduction kernels before any timed call
     for t in range(a.warmup):
         one_step(t)
     # Kernel time: HIP events on the launch stream bracketing the whole timed region (per-launch

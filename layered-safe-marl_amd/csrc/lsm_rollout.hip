@@ -42,7 +42,7 @@
   do {                                                                                       \
     __syncthreads();                                                                         \
     if (lane == 0 && P.stamps) P.stamps[(size_t)env * 16 + (k)] = __builtin_amdgcn_s_memtime(); \
-    if (L.stop_after == (k)) return;  /* per-phase instruction counting (lsm.diag_stamps) */ \
+    if (K.stop_after == (k)) return;  /* per-phase instruction counting (lsm.diag_stamps) */ \
   } while (0)
 // slots 13/14: 100 MHz chip-wide clock at wave start / end (dispatch ramp and tail);
 // slot 15: HW_ID (wave, simd, cu, se) | XCC_ID << 32
@@ -197,6 +197,23 @@ struct LdsPlan {
 
 // q / d for q * d < 2^32 (all index math here): __umulhi(q, ceil(2^32 / d))
 __device__ __forceinline__ int fdiv(int q, uint32_t m) { return (int)__umulhi((uint32_t)q, m); }
+
+// Kernels are specialised on the agent count NT (L = 2, the training setting) so every
+// dimension, LDS offset and index division below folds to a constant; NT = 0 is the
+// generic kernel reading the handle's runtime dimensions.
+#define LSM_DIMS                        \
+  const int N = NT ? NT : P.N;          \
+  const int L = NT ? 2 : P.L;           \
+  const int NL = N * L;                 \
+  const int E = N + NL;                 \
+  const int F = DYN ? 11 : 10;          \
+  (void)L; (void)NL; (void)E; (void)F
+
+// q / d for the small non-negative index math: a constant division when specialised
+template <int NT>
+__device__ __forceinline__ int qdiv(int q, int d, uint32_t m) {
+  return NT ? (int)((uint32_t)q / (uint32_t)d) : fdiv(q, m);
+}
 
 // all() over the LPE-lane group of the calling lane (one env)
 template <int LPE>
@@ -537,10 +554,11 @@ __device__ __forceinline__ bool goal_reached_at(const Lds& S, int N, int NL, int
 // the G partial sums are combined in lane order (float64; ulp-level vs the reference's
 // sequential sum, reward tolerance). Called by ALL lanes; returns the penalty in lanes
 // lane < N (agent = lane), garbage elsewhere.
-template <int LPE>
+template <int LPE, int NT>
 __device__ __forceinline__ double magnetic_penalty_wave(const KParams& P, Lds& S, double* part) {
   const int lane = threadIdx.x & (LPE - 1);
-  const int N = P.N, NL = P.NL;
+  constexpr int DYN = 0;
+  LSM_DIMS;
   int G = 1;
   while (G * 2 * N <= LPE) G *= 2;
   const int a = lane / G, g = lane - a * G;
@@ -638,10 +656,10 @@ __device__ __forceinline__ void rel_state(const Lds& S, int N, int e, int o, dou
   }
 }
 
-template <int DYN>
+template <int DYN, int NT>
 __device__ __forceinline__ void filter_ego(const KParams& P, Lds& S, int i, uint8_t& filtered, int& dec,
                                   double& u0, double& u1) {
-  const int N = P.N;
+  LSM_DIMS;
   u0 = S.raw[i];
   u1 = S.raw[N + i];
   filtered = 0;
@@ -786,9 +804,9 @@ __device__ __forceinline__ void filter_ego(const KParams& P, Lds& S, int i, uint
 // Outputs: per-ego node features + adjacency with the sequential snapshot rule.
 // ego i sees agent j "post" (after its reward update) iff j <= i.
 // ----------------------------------------------------------------------------------
-template <int DYN>
+template <int DYN, int NT>
 __device__ __forceinline__ void node_features(const KParams& P, const Lds& S, int e, int k, float* f) {
-  const int N = P.N, NL = P.NL;
+  LSM_DIMS;
   const double pex = S.ps[e], pey = S.ps[N + e];
   double vex, vey;
   agent_vel<DYN>(S, N, e, true, vex, vey);
@@ -885,10 +903,11 @@ __device__ __forceinline__ uint64_t ego_mask(const Lds& S, int N, int L, int e) 
 
 // DI node features are (entity row) - (ego offset): rows for agents (pre, post update) and
 // landmarks, offsets per ego, built once per step in LDS (utils.py:201-255).
-template <int LPE>
+template <int LPE, int NT>
 __device__ __forceinline__ void build_rows_di(const KParams& P, Lds& S) {
   const int lane = threadIdx.x & (LPE - 1);
-  const int N = P.N, NL = P.NL, F = P.F;
+  constexpr int DYN = 0;
+  LSM_DIMS;
   for (int t = lane; t < 2 * N + NL; t += LPE) {
     double* r = S.feat + (size_t)t * F;
     if (t < 2 * N) {
@@ -921,11 +940,11 @@ __device__ __forceinline__ void build_rows_di(const KParams& P, Lds& S) {
 // pair by one lane, staged in LDS, and copied out as contiguous float4 when the env block is
 // 16-byte aligned; the adjacency is a masked select over the thresholded distance table,
 // one float4 (4 columns of one row) per lane-iteration when E % 4 == 0.
-template <int DYN, int LPE>
+template <int DYN, int LPE, int NT>
 __device__ __forceinline__ void emit_graph(const KParams& P, Lds& S, int env) {
   const int lane = threadIdx.x & (LPE - 1);
-  const int N = P.N, E = P.E, F = P.F;
-  if (DYN == 0) build_rows_di<LPE>(P, S);
+  LSM_DIMS;
+  if (DYN == 0) build_rows_di<LPE, NT>(P, S);
   __syncthreads();
   // No agent changed done / reached status this step (the common case): every ego then has
   // the same disconnect mask and the same (pre == post) entity rows, so each lane computes
@@ -944,7 +963,7 @@ __device__ __forceinline__ void emit_graph(const KParams& P, Lds& S, int env) {
       for (int j = 0; j < 4; ++j) {
         const int t = t0 + j * LPE;
         u[j] = 4 * (t < last ? t : last);
-        const int r = fdiv(u[j], P.m_E);
+        const int r = qdiv<NT>(u[j], E, P.m_E);
         const int c = u[j] - r * E;
         w[j] = *(const float4*)(S.fval + u[j]);
         const uint32_t bits = ((m >> r) & 1ull) ? 0xfu : ((uint32_t)(m >> c) & 0xfu);
@@ -972,7 +991,7 @@ __device__ __forceinline__ void emit_graph(const KParams& P, Lds& S, int env) {
       for (int j = 0; j < 4; ++j) {
         const int t = t0 + j * LPE;
         u[j] = 4 * (t < last ? t : last);
-        rr[j] = fdiv(u[j], P.m_E);
+        rr[j] = qdiv<NT>(u[j], E, P.m_E);
         v[j] = *(const float4*)(S.fval + u[j]);
       }
       for (int e = 0; e < N; ++e) {
@@ -994,9 +1013,9 @@ __device__ __forceinline__ void emit_graph(const KParams& P, Lds& S, int env) {
     }
   } else {
     for (int q = lane; q < atot; q += LPE) {
-      const int e = fdiv(q, P.m_EE);
+      const int e = qdiv<NT>(q, E * E, P.m_EE);
       const int u = q - e * EE;
-      const int r = fdiv(u, P.m_E);
+      const int r = qdiv<NT>(u, E, P.m_E);
       const int c = u - r * E;
       const uint64_t m = S.emask[e];
       adj_out[q] = (((m >> r) | (m >> c)) & 1ull) ? 0.0f : S.fval[u];
@@ -1009,7 +1028,7 @@ __device__ __forceinline__ void emit_graph(const KParams& P, Lds& S, int env) {
     // lane owns float4 t of every ego block: entity rows read once, ego offset per ego
     const int EF4 = E * F / 4;
     for (int t = lane; t < EF4; t += LPE) {
-      int k = fdiv(4 * t, P.m_F);
+      int k = qdiv<NT>(4 * t, F, P.m_F);
       int q = 4 * t - k * F;
       double fv[4];
       int qq[4];
@@ -1033,9 +1052,9 @@ __device__ __forceinline__ void emit_graph(const KParams& P, Lds& S, int env) {
     // contiguous float4 (each ego block is E*F floats, a multiple of 4).
     const int q4 = ntot / 4, EF4 = E * F / 4;
     for (int t = lane; t < q4; t += LPE) {
-      const int e = fdiv(t, P.m_EF4);
+      const int e = qdiv<NT>(t, E * F / 4, P.m_EF4);
       const int j0 = 4 * (t - e * EF4);
-      int k = fdiv(j0, P.m_F);
+      int k = qdiv<NT>(j0, F, P.m_F);
       int q = j0 - k * F;
       const double* o = S.egooff + e * F;
       float f[4];
@@ -1054,7 +1073,7 @@ __device__ __forceinline__ void emit_graph(const KParams& P, Lds& S, int env) {
   for (int b0 = 0; b0 < npairs; b0 += LPE) {
     const int p = b0 + lane;
     if (p < npairs) {
-      const int e = fdiv(p, P.m_E);
+      const int e = qdiv<NT>(p, E, P.m_E);
       const int k = p - e * E;
       float* st = S.stage + lane * F;
       if (DYN == 0) {
@@ -1065,7 +1084,7 @@ __device__ __forceinline__ void emit_graph(const KParams& P, Lds& S, int env) {
         for (int q = 0; q < 10; ++q) st[q] = (float)(r[q] - o[q]);
       } else {
         float f[11];
-        node_features<DYN>(P, S, e, k, f);
+        node_features<DYN, NT>(P, S, e, k, f);
 #pragma unroll
         for (int q = 0; q < 11; ++q) st[q] = f[q];
       }
@@ -1084,10 +1103,11 @@ __device__ __forceinline__ void emit_graph(const KParams& P, Lds& S, int env) {
 
 // cached_dist_mag (core.py:514-543): float32 thresholded copy for the adjacency
 // (adj = d * (d < range) * (d > 0), navigation_graph_safe.py:991-992) + float64 agent block.
-template <int LPE>
+template <int LPE, int NT>
 __device__ __forceinline__ void compute_dist(const KParams& P, Lds& S) {
   const int lane = threadIdx.x & (LPE - 1);
-  const int N = P.N, E = P.E, NL = P.NL;
+  constexpr int DYN = 0;
+  LSM_DIMS;
   const int npair = E * (E - 1) / 2;
   for (int t = lane; t < npair; t += LPE) {
     const uint32_t pr = P.pairs[t];
@@ -1116,12 +1136,12 @@ __device__ __forceinline__ void compute_dist(const KParams& P, Lds& S) {
   __syncthreads();
 }
 
-template <int DYN>
+template <int DYN, int NT>
 __device__ __forceinline__ void write_obs(const KParams& P, const Lds& S, int env, int i) {
-  const int N = P.N, NL = P.NL;
+  LSM_DIMS;
   const int gi = goal_index(S.rpre[i], i, N, NL);
   const double gx = S.lm[gi], gy = S.lm[NL + gi], gh = S.lm[2 * NL + gi], gs = S.lm[3 * NL + gi];
-  float* o = P.o.obs + ((size_t)env * N + i) * P.OBS;
+  float* o = P.o.obs + ((size_t)env * N + i) * (DYN ? 6 : 7);
   const double px = S.ps[i], py = S.ps[N + i];
   if (DYN == 0) {
     o[0] = (float)S.ps[2 * N + i];
@@ -1146,8 +1166,10 @@ __device__ __forceinline__ void write_obs(const KParams& P, const Lds& S, int en
 }
 
 // save_summary_of_episode (environment.py:895-911) from the LDS copy of the stats.
+template <int NT>
 __device__ __forceinline__ void summary(const KParams& P, const Lds& S, double* out) {
-  const int N = P.N;
+  constexpr int DYN = 0;
+  LSM_DIMS;
   const double* tl = S.stats;
   const double* td = S.stats + N;
   const double* dn = S.stats + 2 * N;
@@ -1176,14 +1198,14 @@ __device__ __forceinline__ void summary(const KParams& P, const Lds& S, double* 
 
 // Device reset of one env (MultiAgentGraphEnv.reset, environment.py:1046-1074). Expects the
 // env's persistent per-agent arrays in LDS (S.stats, S.rpost = reached_goal before reset).
-template <int DYN, int LPE>
+template <int DYN, int LPE, int NT>
 __device__ __forceinline__ void reset_env(const KParams& P, Lds& S, int env, const double* cur_new) {
   const int lane = threadIdx.x & (LPE - 1);
-  const int N = P.N, NL = P.NL;
+  LSM_DIMS;
   double* prev = P.s.prev + (size_t)env * 8;
   if (lane == 0) {
     double outv[8];
-    summary(P, S, outv);
+    summary<NT>(P, S, outv);
     for (int k = 0; k < 8; ++k) {
       prev[k] = outv[k];
       P.o.ep_info[(size_t)env * 8 + k] = outv[k];
@@ -1198,7 +1220,7 @@ __device__ __forceinline__ void reset_env(const KParams& P, Lds& S, int env, con
   rng.key = S.mt;
   rng.pos = (int)S.mt[MT_N];
   ScenarioParams sp;
-  sp.dyn = DYN; sp.N = N; sp.L = P.L; sp.world_size = P.world_size; sp.coordination_range = P.coord_range;
+  sp.dyn = DYN; sp.N = N; sp.L = L; sp.world_size = P.world_size; sp.coordination_range = P.coord_range;
   sp.goal_speed_min = P.gs_min; sp.goal_speed_max = P.gs_max;
   sp.ratio_airtaxi = S.cur[C_RAT]; sp.ratio_scenario = S.cur[C_RSC]; sp.two_pi = P.two_pi; sp.pi = P.pi;
   // every lane runs the identical draw sequence and stores the identical values
@@ -1222,9 +1244,9 @@ __device__ __forceinline__ void reset_env(const KParams& P, Lds& S, int env, con
   }
   if (lane == 0) S.step[0] = 0;
   __syncthreads();   // MT words read out of U1 before compute_dist overwrites it
-  compute_dist<LPE>(P, S);
-  if (lane < N) write_obs<DYN>(P, S, env, lane);
-  emit_graph<DYN, LPE>(P, S, env);
+  compute_dist<LPE, NT>(P, S);
+  if (lane < N) write_obs<DYN, NT>(P, S, env, lane);
+  emit_graph<DYN, LPE, NT>(P, S, env);
 }
 
 // Record copy between HBM and the head of the env's LDS block: up to 4 float4 per lane in
@@ -1248,11 +1270,11 @@ __device__ __forceinline__ void rec_copy(const float4* src, float4* dst, int n16
 
 // Persistent record: LDS -> HBM (done agents' velocity / speed stored as zero, core.py
 // freezes them). `full` also writes cur + landmarks (after a reset).
-template <int DYN, int LPE>
+template <int DYN, int LPE, int NT>
 __device__ __forceinline__ void store_state(const KParams& P, Lds& S, const unsigned char* lbase, int env,
                                             bool full) {
   const int lane = threadIdx.x & (LPE - 1);
-  const int N = P.N;
+  LSM_DIMS;
   for (int k = lane; k < 4 * N; k += LPE) {
     const int c = k / N, j = k - c * N;
     double v = S.ps[k];
@@ -1264,8 +1286,8 @@ __device__ __forceinline__ void store_state(const KParams& P, Lds& S, const unsi
   rec_copy<LPE>((const float4*)lbase, P.s.rec + (size_t)env * P.s.rec_stride16, full ? P.s.rec16 : P.s.hot16);
 }
 
-template <int DYN, int LPE>
-__global__ __launch_bounds__(64) void rollout_kernel(const KParams* __restrict__ Pp, const KStep L) {
+template <int DYN, int LPE, int NT>
+__global__ __launch_bounds__(64) void rollout_kernel(const KParams* __restrict__ Pp, const KStep K) {
   const KParams& P = *Pp;   // per-handle constants in device memory; per-launch fields in L
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int G = WAVE / LPE;   // envs per wave, one per LPE-lane group
@@ -1273,9 +1295,9 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams* __restrict__
   const int env = blockIdx.x * G + grp;
   const int lane = threadIdx.x & (LPE - 1);
   if (env >= P.n_envs) return;
-  const int N = P.N, NL = P.NL, E = P.E;
+  LSM_DIMS;
   unsigned char* lbase = smem + (size_t)grp * P.lds_env_bytes;
-  Lds S = carve(lbase, N, NL, E, P.F);
+  Lds S = carve(lbase, N, NL, E, F);
   RTSTAMP(13);
 #ifdef LSM_STAMPS
   if (lane == 0 && P.stamps)
@@ -1286,16 +1308,16 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams* __restrict__
 
   // ---- 0. the env's record HBM -> LDS (one round trip) + this step's actions ------------
   int ai = 0;
-  if (L.mode == 0 && lane < N) {
+  if (K.mode == 0 && lane < N) {
     const size_t base = (size_t)env * N + lane;
-    if (L.action_kind == LSM_ACTIONS_INDEX_I32) {
-      ai = ((const int32_t*)L.actions)[base];
-    } else if (L.action_kind == LSM_ACTIONS_ONEHOT_F32) {
-      const float* a = (const float*)L.actions + base * 25;
+    if (K.action_kind == LSM_ACTIONS_INDEX_I32) {
+      ai = ((const int32_t*)K.actions)[base];
+    } else if (K.action_kind == LSM_ACTIONS_ONEHOT_F32) {
+      const float* a = (const float*)K.actions + base * 25;
       float best = a[0];
       for (int q = 1; q < 25; ++q) if (a[q] > best) { best = a[q]; ai = q; }
     } else {
-      const double* a = (const double*)L.actions + base * 25;
+      const double* a = (const double*)K.actions + base * 25;
       double best = a[0];
       for (int q = 1; q < 25; ++q) if (a[q] > best) { best = a[q]; ai = q; }
     }
@@ -1310,19 +1332,19 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams* __restrict__
   __syncthreads();
   STAMP(1);
 
-  if (L.mode == 1) {
-    reset_env<DYN, LPE>(P, S, env, L.cur_new);
+  if (K.mode == 1) {
+    reset_env<DYN, LPE, NT>(P, S, env, K.cur_new);
     __syncthreads();
-    store_state<DYN, LPE>(P, S, lbase, env, true);
+    store_state<DYN, LPE, NT>(P, S, lbase, env, true);
     return;
   }
 
   // ---- 1. update_graph() at step start (previous state, final masks) --------------
-  if (L.emit_edges) {
+  if (K.emit_edges) {
     uint8_t* eo = P.o.edges + (size_t)env * E * E;
-    const uint64_t m0 = ego_mask(S, N, P.L, N);
+    const uint64_t m0 = ego_mask(S, N, L, N);
     for (int u = lane; u < E * E; u += LPE) {
-      const int a = fdiv(u, P.m_E), b = u - a * E;
+      const int a = qdiv<NT>(u, E, P.m_E), b = u - a * E;
       double d = 0.0;
       if (a != b) {
         const int lo = a < b ? a : b, hi = a < b ? b : a;
@@ -1374,7 +1396,7 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams* __restrict__
     if (filter_on) {
       uint8_t fl = 0;
       int dec = -1;
-      if (!S.dpre[i]) filter_ego<DYN>(P, S, i, fl, dec, u0, u1);
+      if (!S.dpre[i]) filter_ego<DYN, NT>(P, S, i, fl, dec, u0, u1);
       S.sfilt[i] = fl;
       S.decon[i] = dec;
     }
@@ -1437,7 +1459,7 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams* __restrict__
   STAMP(5);
 
   // ---- 5. distances, min relative distance ---------------------------------------------
-  compute_dist<LPE>(P, S);
+  compute_dist<LPE, NT>(P, S);
   if (lane < N) {
     const int i = lane;
     double m = INFINITY;
@@ -1454,13 +1476,13 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams* __restrict__
 
   // ---- 6. obs, reward, goal/done update ---------------------------------------------------
   double mag = 0.0;
-  if (DYN == 0 && !P.use_filter_arg) mag = magnetic_penalty_wave<LPE>(P, S, S.dpair);
+  if (DYN == 0 && !P.use_filter_arg) mag = magnetic_penalty_wave<LPE, NT>(P, S, S.dpair);
   double rew = 0.0;
   double th_pre = 0.0, spd_pre = 0.0;
   bool reached_pre = false;
   if (lane < N) {
     const int i = lane;
-    write_obs<DYN>(P, S, env, i);
+    write_obs<DYN, NT>(P, S, env, i);
     const int gi = goal_index(S.rpre[i], i, N, NL);
     const double gx = S.lm[gi], gy = S.lm[NL + gi], gh = S.lm[2 * NL + gi], gs = S.lm[3 * NL + gi];
     const double px = S.ps[i], py = S.ps[N + i];
@@ -1514,11 +1536,11 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams* __restrict__
     int rp = S.rpre[i];
     if (reached && (!P.use_masking || !done0)) rp += 1;
     S.rpost[i] = rp;
-    S.dpost[i] = (rp >= P.L) ? 1 : S.dpre[i];
+    S.dpost[i] = (rp >= L) ? 1 : S.dpre[i];
     P.o.rew[(size_t)env * N + i] = (float)rew;
   }
   __syncthreads();
-  if (lane < N) S.emask[lane] = ego_mask(S, N, P.L, lane);
+  if (lane < N) S.emask[lane] = ego_mask(S, N, L, lane);
   STAMP(7);
 
   // ---- 7/8. info_callback numbers -----------------------------------------------------
@@ -1628,16 +1650,16 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams* __restrict__
   if (lane == 0) S.step[0] = cstep;
   if (P.auto_reset && all_done) {
     if (lane == 0) P.o.reset_flag[env] = 1;
-    reset_env<DYN, LPE>(P, S, env, L.cur_new);
+    reset_env<DYN, LPE, NT>(P, S, env, K.cur_new);
     __syncthreads();
     STAMP(12);
-    store_state<DYN, LPE>(P, S, lbase, env, true);
+    store_state<DYN, LPE, NT>(P, S, lbase, env, true);
   } else {
     if (lane == 0) P.o.reset_flag[env] = 0;
-    emit_graph<DYN, LPE>(P, S, env);
+    emit_graph<DYN, LPE, NT>(P, S, env);
     __syncthreads();
     STAMP(10);
-    store_state<DYN, LPE>(P, S, lbase, env, false);
+    store_state<DYN, LPE, NT>(P, S, lbase, env, false);
   }
   STAMP(11);
   RTSTAMP(14);
@@ -1675,7 +1697,8 @@ struct lsm_env {
   int device;
   KParams* dparams;   // device copy of the per-handle constants (re-uploaded when dirty)
   bool params_dirty;
-  int lpe;   // lanes per env: 64 (one env per wave), 32 or 16 (2 or 4 envs per wave)
+  int lpe;   // lanes per env
+  bool generic_only;   // LSM_GENERIC=1: never use the compile-time-N kernels (tests): 64 (one env per wave), 32 or 16 (2 or 4 envs per wave)
 };
 
 static int fail(lsm_env* e, const std::string& msg) {
@@ -1821,6 +1844,7 @@ int lsm_create(const lsm_config* cfg, lsm_env** out) {
   // instruction stream (needs N <= lanes). LSM_LPE overrides.
   e->lpe = 64;
   if (const char* v = getenv("LSM_LPE")) e->lpe = atoi(v);
+  e->generic_only = getenv("LSM_GENERIC") && atoi(getenv("LSM_GENERIC")) != 0;
   if (!(e->lpe == 16 || e->lpe == 32 || e->lpe == 64) || e->lpe < N)
     return fail(e, "LSM_LPE must be 16, 32 or 64 and >= num_agents");
   HIPCHK(e, hipGetDevice(&e->device));
@@ -1978,11 +2002,11 @@ static int check_ready(lsm_env* e, bool stepping) {
   return 0;
 }
 
-extern "C++" template <int DYN, int LPE>
+extern "C++" template <int DYN, int LPE, int NT>
 static void launch_t(lsm_env* e, const KStep& L, size_t env_lds, hipStream_t st) {
   constexpr int G = WAVE / LPE;
   const int blocks = (e->cfg.num_envs + G - 1) / G;
-  hipLaunchKernelGGL((rollout_kernel<DYN, LPE>), dim3(blocks), dim3(WAVE), env_lds * G, st,
+  hipLaunchKernelGGL((rollout_kernel<DYN, LPE, NT>), dim3(blocks), dim3(WAVE), env_lds * G, st,
                      (const KParams*)e->dparams, L);
 }
 
@@ -2001,15 +2025,25 @@ static int launch(lsm_env* e, KStep& L, hipStream_t st) {
 #ifdef LSM_STAMPS
   if (const char* v = getenv("LSM_STOP_AFTER")) L.stop_after = atoi(v);
 #endif
-  const int k = (e->cfg.dynamics ? 4 : 0) + (e->lpe == 64 ? 0 : e->lpe == 32 ? 1 : e->lpe == 16 ? 2 : 3);
-  switch (k) {
-    case 0: launch_t<0, 64>(e, L, env_lds, st); break;
-    case 1: launch_t<0, 32>(e, L, env_lds, st); break;
-    case 2: launch_t<0, 16>(e, L, env_lds, st); break;
-    case 4: launch_t<1, 64>(e, L, env_lds, st); break;
-    case 5: launch_t<1, 32>(e, L, env_lds, st); break;
-    case 6: launch_t<1, 16>(e, L, env_lds, st); break;
-    default: return fail(e, "unsupported lanes-per-env");
+  // specialised kernels (compile-time N, L = 2, one env per wave) for the BASELINE agent
+  // counts; everything else runs the generic kernel (runtime dims, LPE 64/32/16)
+  const bool spec = e->lpe == 64 && e->L == 2 && !e->generic_only;
+  const bool di = e->cfg.dynamics == LSM_DOUBLE_INTEGRATOR;
+  if (spec && di && e->N == 3) launch_t<0, 64, 3>(e, L, env_lds, st);
+  else if (spec && di && e->N == 8) launch_t<0, 64, 8>(e, L, env_lds, st);
+  else if (spec && !di && e->N == 3) launch_t<1, 64, 3>(e, L, env_lds, st);
+  else if (spec && !di && e->N == 16) launch_t<1, 64, 16>(e, L, env_lds, st);
+  else {
+    const int k = (di ? 0 : 4) + (e->lpe == 64 ? 0 : e->lpe == 32 ? 1 : e->lpe == 16 ? 2 : 3);
+    switch (k) {
+      case 0: launch_t<0, 64, 0>(e, L, env_lds, st); break;
+      case 1: launch_t<0, 32, 0>(e, L, env_lds, st); break;
+      case 2: launch_t<0, 16, 0>(e, L, env_lds, st); break;
+      case 4: launch_t<1, 64, 0>(e, L, env_lds, st); break;
+      case 5: launch_t<1, 32, 0>(e, L, env_lds, st); break;
+      case 6: launch_t<1, 16, 0>(e, L, env_lds, st); break;
+      default: return fail(e, "unsupported lanes-per-env");
+    }
   }
   HIPCHK(e, hipGetLastError());
   return 0;

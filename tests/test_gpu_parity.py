@@ -107,11 +107,15 @@ CASES = [
 ]
 
 
-@pytest.mark.parametrize("lpe", [16, 32, 64])
+@pytest.mark.parametrize("lpe", [16, 32, 64, "64g"])
 @pytest.mark.parametrize("case", range(len(CASES)))
 def test_gpu_matches_oracle_multi_env(case, lpe, monkeypatch):
     """16 (or 15: a partly filled last wave) envs with per-env seeds seed + 1000 k, random
-    actions, across an auto-reset; every lanes-per-env kernel variant (1, 2 or 4 envs/wave)."""
+    actions, across an auto-reset; every kernel variant: 1, 2 or 4 envs/wave, and at one env
+    per wave both the compile-time-N kernel (N = 3, 8, 16) and the generic one ("64g")."""
+    if lpe == "64g":
+        monkeypatch.setenv("LSM_GENERIC", "1")
+        lpe = 64
     monkeypatch.setenv("LSM_LPE", str(lpe))
     c = dict(CASES[case])
     ep = c.pop("ep")
