@@ -41,14 +41,14 @@
 #define STAMP(k)                                                                             \
   do {                                                                                       \
     __syncthreads();                                                                         \
-    if (lane == 0 && P.stamps) P.stamps[(size_t)env * 16 + (k)] = __builtin_amdgcn_s_memtime(); \
+    if (lane == 0 && gptr(P.stamps)) gptr(P.stamps)[(size_t)env * 16 + (k)] = __builtin_amdgcn_s_memtime(); \
     if (K.stop_after == (k)) return;  /* per-phase instruction counting (lsm.diag_stamps) */ \
   } while (0)
 // slots 13/14: 100 MHz chip-wide clock at wave start / end (dispatch ramp and tail);
 // slot 15: HW_ID (wave, simd, cu, se) | XCC_ID << 32
 #define RTSTAMP(k)                                                                           \
   do {                                                                                       \
-    if (lane == 0 && P.stamps) P.stamps[(size_t)env * 16 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+    if (lane == 0 && gptr(P.stamps)) gptr(P.stamps)[(size_t)env * 16 + (k)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
 #else
 #define RTSTAMP(k) \
@@ -127,6 +127,7 @@ struct KParams {
   double ttr_max;
   uint32_t m_E, m_EE, m_EF, m_F, m_EF4;  // ceil(2^32 / d) for exact small-numerator division
   unsigned long long* stamps;     // LSM_OUT_DEBUG_STAMPS (diagnostic builds only)
+  int diag;                       // diagnostic builds: bit 0 = skip adj/node stores (LSM_DIAG)
   uint32_t lds_env_bytes;         // LDS bytes per env (envs per wave > 1: consecutive blocks)
   const uint16_t* pairs;          // strict upper-triangle entity pairs (a | b << 8)
   TableDev val, ttr;
@@ -215,13 +216,30 @@ __device__ __forceinline__ int qdiv(int q, int d, uint32_t m) {
   return NT ? (int)((uint32_t)q / (uint32_t)d) : fdiv(q, m);
 }
 
+// Pointers read from the device-resident KParams are generic; re-tagging them as global
+// (address space 1) lets the compiler emit global_* instead of flat_* accesses (flat
+// stores also count against lgkmcnt, so every later LDS wait would drain them).
+#define GAS __attribute__((address_space(1)))
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+template <class T>
+__device__ __forceinline__ GAS T* gptr(T* p) {
+  return (GAS T*)p;
+}
+
+// One float4 of the per-step graph outputs. (Non-temporal stores were measured slower with
+// the filter on: 37.9 vs 35.9 us per step at config 3.)
+__device__ __forceinline__ void st_stream(GAS float* dst, float4 v) {
+  const f32x4 x = {v.x, v.y, v.z, v.w};
+  *(GAS f32x4*)dst = x;
+}
+
 // all() over the LPE-lane group of the calling lane (one env)
 template <int LPE>
 __device__ __forceinline__ bool group_all(bool v) {
   if (LPE == 64) return __all(v);
   const uint64_t b = __ballot(v);
   const int g = (int)threadIdx.x / LPE;
-  const uint64_t gm = ((1ull << LPE) - 1) << (g * LPE);
+  const uint64_t gm = (~0ull >> (64 - LPE)) << (g * LPE);
   return (b & gm) == gm;
 }
 
@@ -407,11 +425,11 @@ __device__ __forceinline__ bool interp_value(const TableDev& T, const double* s,
   int cell;
   float w[1 << ND];
   if (!grid_cell<ND>(T, s, cell, w)) return false;
-  const float4* c4 = (const float4*)(T.cells + (size_t)cell * (1 << ND));
+  const GAS f32x4* c4 = (const GAS f32x4*)(gptr(T.cells) + (size_t)cell * (1 << ND));
   float v[1 << ND];
 #pragma unroll
   for (int q = 0; q < (1 << ND) / 4; ++q) {
-    const float4 x = c4[q];
+    const f32x4 x = c4[q];
     v[4 * q] = x.x; v[4 * q + 1] = x.y; v[4 * q + 2] = x.z; v[4 * q + 3] = x.w;
   }
   float acc = 0.0f;
@@ -430,13 +448,13 @@ __device__ __forceinline__ void interp_grad(const TableDev& T, const double* s, 
     for (int d = 0; d < ND; ++d) g[d] = __builtin_nanf("");
     return;
   }
-  const float4* gc = T.gcells + (size_t)cell * (1 << ND) * T.gw;
+  const GAS f32x4* gc = (const GAS f32x4*)gptr(T.gcells) + (size_t)cell * (1 << ND) * T.gw;
 #pragma unroll
   for (int c = 0; c < (1 << ND); ++c) {
-    const float4 a = gc[c * T.gw];
+    const f32x4 a = gc[c * T.gw];
     float gv[8] = {a.x, a.y, a.z, a.w, 0.f, 0.f, 0.f, 0.f};
     if (ND > 4) {
-      const float4 b = gc[c * T.gw + 1];
+      const f32x4 b = gc[c * T.gw + 1];
       gv[4] = b.x; gv[5] = b.y; gv[6] = b.z; gv[7] = b.w;
     }
 #pragma unroll
@@ -506,17 +524,6 @@ __device__ __forceinline__ double agent_speed(const Lds& S, int N, int j, bool p
     return sqrt(vx * vx + vy * vy);
   }
   return frozen ? 0.0 : S.ps[3 * N + j];
-}
-
-template <int DYN>
-__device__ __forceinline__ double agent_theta(const Lds& S, int N, int j, bool post) {
-  if (DYN == 0) {
-    const bool frozen = post && S.dpost[j];
-    const double vx = frozen ? 0.0 : S.ps[2 * N + j];
-    const double vy = frozen ? 0.0 : S.ps[3 * N + j];
-    return atan2(vy, vx);
-  }
-  return S.ps[2 * N + j];
 }
 
 // evaluate_agent_goal_reached (navigation_graph_safe.py:606-656) for goal gi, given the
@@ -952,7 +959,7 @@ __device__ __forceinline__ void emit_graph(const KParams& P, Lds& S, int env) {
   const bool uni = group_all<LPE>(lane >= N || (S.dpre[lane] == S.dpost[lane] && S.rpre[lane] == S.rpost[lane]));
   // ---- adjacency: ego e, row r, col c ------------------------------------------------------
   const int EE = E * E, atot = N * EE;
-  float* adj_out = P.o.adj + (size_t)env * atot;
+  GAS float* adj_out = gptr(P.o.adj) + (size_t)env * atot;
   if ((E & 3) == 0 && uni) {
     const int Q = EE / 4, last = Q - 1;
     const uint64_t m = S.emask[0];
@@ -972,11 +979,14 @@ __device__ __forceinline__ void emit_graph(const KParams& P, Lds& S, int env) {
         if (bits & 4u) w[j].z = 0.f;
         if (bits & 8u) w[j].w = 0.f;
       }
+#ifdef LSM_STAMPS
+      if (P.diag & 1) continue;
+#endif
       for (int e = 0; e < N; ++e) {
-        float* dst = adj_out + (size_t)e * EE;
+        GAS float* dst = adj_out + (size_t)e * EE;
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          if (t0 + j * LPE <= last) *(float4*)(dst + u[j]) = w[j];
+          if (t0 + j * LPE <= last) st_stream(dst + u[j], w[j]);
       }
     }
   } else if ((E & 3) == 0) {
@@ -996,7 +1006,7 @@ __device__ __forceinline__ void emit_graph(const KParams& P, Lds& S, int env) {
       }
       for (int e = 0; e < N; ++e) {
         const uint64_t m = S.emask[e];
-        float* dst = adj_out + (size_t)e * EE;
+        GAS float* dst = adj_out + (size_t)e * EE;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           if (t0 + j * LPE > last) break;
@@ -1007,7 +1017,7 @@ __device__ __forceinline__ void emit_graph(const KParams& P, Lds& S, int env) {
           if (bits & 2u) w.y = 0.f;
           if (bits & 4u) w.z = 0.f;
           if (bits & 8u) w.w = 0.f;
-          *(float4*)(dst + u[j]) = w;
+          st_stream(dst + u[j], w);
         }
       }
     }
@@ -1023,7 +1033,7 @@ __device__ __forceinline__ void emit_graph(const KParams& P, Lds& S, int env) {
   }
   // ---- node features --------------------------------------------------------------
   const int npairs = N * E, ntot = npairs * F;
-  float* node_out = P.o.node + (size_t)env * ntot;
+  GAS float* node_out = gptr(P.o.node) + (size_t)env * ntot;
   if (DYN == 0 && ((E * F) & 3) == 0 && uni) {
     // lane owns float4 t of every ego block: entity rows read once, ego offset per ego
     const int EF4 = E * F / 4;
@@ -1038,11 +1048,14 @@ __device__ __forceinline__ void emit_graph(const KParams& P, Lds& S, int env) {
         qq[c] = q;
         if (++q == F) { q = 0; ++k; }
       }
+#ifdef LSM_STAMPS
+      if (P.diag & 1) continue;
+#endif
       for (int e = 0; e < N; ++e) {
         const double* o = S.egooff + e * F;
-        *(float4*)(node_out + (size_t)e * E * F + 4 * t) =
+        st_stream(node_out + (size_t)e * E * F + 4 * t,
             make_float4((float)(fv[0] - o[qq[0]]), (float)(fv[1] - o[qq[1]]), (float)(fv[2] - o[qq[2]]),
-                        (float)(fv[3] - o[qq[3]]));
+                        (float)(fv[3] - o[qq[3]])));
       }
     }
     return;
@@ -1091,9 +1104,9 @@ __device__ __forceinline__ void emit_graph(const KParams& P, Lds& S, int env) {
     }
     __syncthreads();
     const int cnt = min(LPE, npairs - b0) * F;
-    float* dst = node_out + (size_t)b0 * F;
+    GAS float* dst = node_out + (size_t)b0 * F;
     if (nvec && (cnt & 3) == 0) {
-      for (int q = lane; q < cnt / 4; q += LPE) ((float4*)dst)[q] = ((const float4*)S.stage)[q];
+      for (int q = lane; q < cnt / 4; q += LPE) ((GAS f32x4*)dst)[q] = ((const f32x4*)S.stage)[q];
     } else {
       for (int q = lane; q < cnt; q += LPE) dst[q] = S.stage[q];
     }
@@ -1110,7 +1123,7 @@ __device__ __forceinline__ void compute_dist(const KParams& P, Lds& S) {
   LSM_DIMS;
   const int npair = E * (E - 1) / 2;
   for (int t = lane; t < npair; t += LPE) {
-    const uint32_t pr = P.pairs[t];
+    const uint32_t pr = gptr(P.pairs)[t];
     const int a = (int)(pr & 0xffu), b = (int)(pr >> 8);
     const double xa = a < N ? S.ps[a] : S.lm[a - N];
     const double ya = a < N ? S.ps[N + a] : S.lm[NL + a - N];
@@ -1141,7 +1154,7 @@ __device__ __forceinline__ void write_obs(const KParams& P, const Lds& S, int en
   LSM_DIMS;
   const int gi = goal_index(S.rpre[i], i, N, NL);
   const double gx = S.lm[gi], gy = S.lm[NL + gi], gh = S.lm[2 * NL + gi], gs = S.lm[3 * NL + gi];
-  float* o = P.o.obs + ((size_t)env * N + i) * (DYN ? 6 : 7);
+  GAS float* o = gptr(P.o.obs) + ((size_t)env * N + i) * (DYN ? 6 : 7);
   const double px = S.ps[i], py = S.ps[N + i];
   if (DYN == 0) {
     o[0] = (float)S.ps[2 * N + i];
@@ -1202,18 +1215,18 @@ template <int DYN, int LPE, int NT>
 __device__ __forceinline__ void reset_env(const KParams& P, Lds& S, int env, const double* cur_new) {
   const int lane = threadIdx.x & (LPE - 1);
   LSM_DIMS;
-  double* prev = P.s.prev + (size_t)env * 8;
+  GAS double* prev = gptr(P.s.prev) + (size_t)env * 8;
   if (lane == 0) {
     double outv[8];
     summary<NT>(P, S, outv);
     for (int k = 0; k < 8; ++k) {
       prev[k] = outv[k];
-      P.o.ep_info[(size_t)env * 8 + k] = outv[k];
+      gptr(P.o.ep_info)[(size_t)env * 8 + k] = outv[k];
     }
   }
   __syncthreads();
   for (int k = lane; k < NCUR; k += LPE) S.cur[k] = cur_new[k];
-  const uint32_t* mtg = P.s.mt + (size_t)env * MT_WORDS;
+  const GAS uint32_t* mtg = gptr(P.s.mt) + (size_t)env * MT_WORDS;
   for (int k = lane; k < MT_WORDS; k += LPE) S.mt[k] = mtg[k];
   __syncthreads();
   WaveRng<LPE> rng;
@@ -1228,7 +1241,7 @@ __device__ __forceinline__ void reset_env(const KParams& P, Lds& S, int env, con
   __syncthreads();
   if (lane == 0) S.mt[MT_N] = (uint32_t)rng.pos;
   __syncthreads();
-  uint32_t* mtw = P.s.mt + (size_t)env * MT_WORDS;
+  GAS uint32_t* mtw = gptr(P.s.mt) + (size_t)env * MT_WORDS;
   for (int k = lane; k < MT_WORDS; k += LPE) mtw[k] = S.mt[k];
   for (int k = lane; k < NL; k += LPE) {
     S.lmsc[k] = sin(S.lm[2 * NL + k]);
@@ -1251,16 +1264,16 @@ __device__ __forceinline__ void reset_env(const KParams& P, Lds& S, int env, con
 
 // Record copy between HBM and the head of the env's LDS block: up to 4 float4 per lane in
 // flight before the first write, so a record of <= 4 KB costs one round trip.
-template <int LPE>
-__device__ __forceinline__ void rec_copy(const float4* src, float4* dst, int n16) {
+template <int LPE, class SP, class DP>
+__device__ __forceinline__ void rec_copy(SP src, DP dst, int n16) {
   const int lane = threadIdx.x & (LPE - 1);
   for (int k0 = lane; k0 < n16; k0 += 4 * LPE) {
     const int k1 = k0 + LPE, k2 = k0 + 2 * LPE, k3 = k0 + 3 * LPE;
     const int last = n16 - 1;   // clamped (always in-bounds) loads, predicated stores
-    const float4 r0 = src[k0];
-    const float4 r1 = src[k1 < last ? k1 : last];
-    const float4 r2 = src[k2 < last ? k2 : last];
-    const float4 r3 = src[k3 < last ? k3 : last];
+    const f32x4 r0 = src[k0];
+    const f32x4 r1 = src[k1 < last ? k1 : last];
+    const f32x4 r2 = src[k2 < last ? k2 : last];
+    const f32x4 r3 = src[k3 < last ? k3 : last];
     dst[k0] = r0;
     if (k1 < n16) dst[k1] = r1;
     if (k2 < n16) dst[k2] = r2;
@@ -1280,10 +1293,10 @@ __device__ __forceinline__ void store_state(const KParams& P, Lds& S, const unsi
     double v = S.ps[k];
     if (S.dpost[j] && (DYN == 0 ? (c >= 2) : (c == 3))) v = 0.0;
     S.ps[k] = v;
-    if (P.o.state) P.o.state[((size_t)env * N + j) * 4 + c] = v;
+    if (P.o.state) gptr(P.o.state)[((size_t)env * N + j) * 4 + c] = v;
   }
   __syncthreads();
-  rec_copy<LPE>((const float4*)lbase, P.s.rec + (size_t)env * P.s.rec_stride16, full ? P.s.rec16 : P.s.hot16);
+  rec_copy<LPE>((const f32x4*)lbase, (GAS f32x4*)gptr(P.s.rec) + (size_t)env * P.s.rec_stride16, full ? P.s.rec16 : P.s.hot16);
 }
 
 template <int DYN, int LPE, int NT>
@@ -1300,8 +1313,8 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams* __restrict__
   Lds S = carve(lbase, N, NL, E, F);
   RTSTAMP(13);
 #ifdef LSM_STAMPS
-  if (lane == 0 && P.stamps)
-    P.stamps[(size_t)env * 16 + 15] = (unsigned long long)__builtin_amdgcn_s_getreg(63492) |
+  if (lane == 0 && gptr(P.stamps))
+    gptr(P.stamps)[(size_t)env * 16 + 15] = (unsigned long long)__builtin_amdgcn_s_getreg(63492) |
                                       ((unsigned long long)__builtin_amdgcn_s_getreg(6164) << 32);
 #endif
   STAMP(0);
@@ -1311,18 +1324,18 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams* __restrict__
   if (K.mode == 0 && lane < N) {
     const size_t base = (size_t)env * N + lane;
     if (K.action_kind == LSM_ACTIONS_INDEX_I32) {
-      ai = ((const int32_t*)K.actions)[base];
+      ai = ((const GAS int32_t*)gptr(K.actions))[base];
     } else if (K.action_kind == LSM_ACTIONS_ONEHOT_F32) {
-      const float* a = (const float*)K.actions + base * 25;
+      const GAS float* a = (const GAS float*)gptr(K.actions) + base * 25;
       float best = a[0];
       for (int q = 1; q < 25; ++q) if (a[q] > best) { best = a[q]; ai = q; }
     } else {
-      const double* a = (const double*)K.actions + base * 25;
+      const GAS double* a = (const GAS double*)gptr(K.actions) + base * 25;
       double best = a[0];
       for (int q = 1; q < 25; ++q) if (a[q] > best) { best = a[q]; ai = q; }
     }
   }
-  rec_copy<LPE>(P.s.rec + (size_t)env * P.s.rec_stride16, (float4*)lbase, P.s.rec16);
+  rec_copy<LPE>((const GAS f32x4*)gptr(P.s.rec) + (size_t)env * P.s.rec_stride16, (f32x4*)lbase, P.s.rec16);
   __syncthreads();
   if (lane < N) {
     S.dpre[lane] = S.dpost[lane];
@@ -1341,7 +1354,7 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams* __restrict__
 
   // ---- 1. update_graph() at step start (previous state, final masks) --------------
   if (K.emit_edges) {
-    uint8_t* eo = P.o.edges + (size_t)env * E * E;
+    GAS uint8_t* eo = gptr(P.o.edges) + (size_t)env * E * E;
     const uint64_t m0 = ego_mask(S, N, L, N);
     for (int u = lane; u < E * E; u += LPE) {
       const int a = qdiv<NT>(u, E, P.m_E), b = u - a * E;
@@ -1478,7 +1491,7 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams* __restrict__
   double mag = 0.0;
   if (DYN == 0 && !P.use_filter_arg) mag = magnetic_penalty_wave<LPE, NT>(P, S, S.dpair);
   double rew = 0.0;
-  double th_pre = 0.0, spd_pre = 0.0;
+  double th_pre = 0.0, spd_pre = 0.0, ct_pre = 1.0, st_pre = 0.0;
   bool reached_pre = false;
   if (lane < N) {
     const int i = lane;
@@ -1486,10 +1499,24 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams* __restrict__
     const int gi = goal_index(S.rpre[i], i, N, NL);
     const double gx = S.lm[gi], gy = S.lm[NL + gi], gh = S.lm[2 * NL + gi], gs = S.lm[3 * NL + gi];
     const double px = S.ps[i], py = S.ps[N + i];
-    th_pre = agent_theta<DYN>(S, N, i, false);
     spd_pre = agent_speed<DYN>(S, N, i, false);
-    const double th = th_pre, spd = spd_pre;
-    const double he = dae(th, gh);
+    const double spd = spd_pre;
+    double he;
+    if (DYN == 0) {
+      // DI heading = atan2(vy, vx) (atan2(0, 0) = 0): its cos / sin are v / |v|, so
+      // direction_alignment_error = 0.5 - 0.5 cos(th - gh) needs no atan2 / cos (ulp-level
+      // vs the reference, like the integrator); goal sin / cos are cached per episode
+      if (spd > 0.0) {
+        const double inv = 1.0 / spd;
+        ct_pre = S.ps[2 * N + i] * inv;
+        st_pre = S.ps[3 * N + i] * inv;
+      }
+      he = 0.5 - 0.5 * (ct_pre * S.lmsc[NL + gi] + st_pre * S.lmsc[gi]);
+    } else {
+      th_pre = S.ps[2 * N + i];
+      he = dae(th_pre, gh);
+    }
+    const double th = th_pre;
     const double hpr = 1 - np_clip(he / S.cur[C_GHE], 0, 1);
     const double se = fabs(spd - gs);
     const double sen = np_clip(se / S.cur[C_GSE], 0, 1);
@@ -1501,7 +1528,7 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams* __restrict__
     if (reached) {
       const double spr = 1 - sen;
       const double ddx = gx - px, ddy = gy - py;
-      double cte = ddx * sin(th) - ddy * cos(th);
+      double cte = (DYN == 0) ? ddx * st_pre - ddy * ct_pre : ddx * sin(th) - ddy * cos(th);
       cte = fabs(cte) / np_maximum(blas_norm2(ddx, ddy), 1e-6);
       const double ctp = 1 - np_clip(cte, 0, 1);
       const double perf = hpr * spr * ctp;
@@ -1518,7 +1545,7 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams* __restrict__
         r = P.use_filter_arg ? r - 1.0 : r - 1.0 * S.cur[C_SLOPED];
       } else {
         double rpx, rpy;
-        blas_rot(cos(gh), sin(gh), px - gx, py - gy, rpx, rpy);
+        blas_rot(S.lmsc[NL + gi], S.lmsc[gi], px - gx, py - gy, rpx, rpy);   // cached cos / sin(gh)
         const double rs[4] = {rpx, rpy, th - gh, spd};
         float ttr = 0.0f;
         if (interp_value<4>(P.ttr, rs, ttr)) {
@@ -1537,7 +1564,7 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams* __restrict__
     if (reached && (!P.use_masking || !done0)) rp += 1;
     S.rpost[i] = rp;
     S.dpost[i] = (rp >= L) ? 1 : S.dpre[i];
-    P.o.rew[(size_t)env * N + i] = (float)rew;
+    gptr(P.o.rew)[(size_t)env * N + i] = (float)rew;
   }
   __syncthreads();
   if (lane < N) S.emask[lane] = ego_mask(S, N, L, lane);
@@ -1555,9 +1582,15 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams* __restrict__
     bool reached_post = reached_pre;   // same state and goal unless the goal advanced
     if (S.rpost[i] != S.rpre[i]) {
       const bool frz = S.dpost[i] != 0;
-      const double thp = frz ? (DYN == 0 ? 0.0 : th_pre) : th_pre;   // atan2(0, 0) = 0
       const double spp = frz ? 0.0 : spd_pre;
-      reached_post = goal_reached_at<DYN>(S, N, NL, i, gi, spp, dae(thp, S.lm[2 * NL + gi]));
+      double hep;
+      if (DYN == 0) {   // frozen: zero velocity, atan2(0, 0) = 0
+        const double c = frz ? 1.0 : ct_pre, sn = frz ? 0.0 : st_pre;
+        hep = 0.5 - 0.5 * (c * S.lmsc[NL + gi] + sn * S.lmsc[gi]);
+      } else {
+        hep = dae(th_pre, S.lm[2 * NL + gi]);
+      }
+      reached_post = goal_reached_at<DYN>(S, N, NL, i, gi, spp, hep);
     }
     if (reached_post && tr == -1) {
       tr = cstep * P.dt;
@@ -1608,7 +1641,7 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams* __restrict__
     inf[LSM_INFO_REACHED_GOAL] = (double)S.rpost[i];
   }
   __syncthreads();
-  rec_copy<LPE>((const float4*)S.dpair, (float4*)(P.o.info + (size_t)env * N * LSM_INFO_FIELDS),
+  rec_copy<LPE>((const f32x4*)S.dpair, (GAS f32x4*)(gptr(P.o.info) + (size_t)env * N * LSM_INFO_FIELDS),
                 N * LSM_INFO_FIELDS / 2);
   STAMP(8);
 
@@ -1640,7 +1673,7 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams* __restrict__
     }
     if (S.dpost[i]) S.stats[2 * N + i] = 1;
     my_done = S.dpost[i] || cstep >= P.episode_length;
-    P.o.dones[(size_t)env * N + i] = my_done ? 1 : 0;
+    gptr(P.o.dones)[(size_t)env * N + i] = my_done ? 1 : 0;
   }
   const bool all_done = group_all<LPE>(my_done);
   __syncthreads();
@@ -1649,13 +1682,13 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams* __restrict__
   // ---- 9. graph outputs, or the auto-reset (whose outputs replace them) ---------------------
   if (lane == 0) S.step[0] = cstep;
   if (P.auto_reset && all_done) {
-    if (lane == 0) P.o.reset_flag[env] = 1;
+    if (lane == 0) gptr(P.o.reset_flag)[env] = 1;
     reset_env<DYN, LPE, NT>(P, S, env, K.cur_new);
     __syncthreads();
     STAMP(12);
     store_state<DYN, LPE, NT>(P, S, lbase, env, true);
   } else {
-    if (lane == 0) P.o.reset_flag[env] = 0;
+    if (lane == 0) gptr(P.o.reset_flag)[env] = 0;
     emit_graph<DYN, LPE, NT>(P, S, env);
     __syncthreads();
     STAMP(10);
@@ -1786,6 +1819,10 @@ static void fill_params(const lsm_env* e, KParams& P) {
   P.o.edges = (uint8_t*)e->out_ptr[LSM_OUT_EDGES];
   P.o.state = (double*)e->out_ptr[LSM_OUT_STATE];
   P.stamps = (unsigned long long*)e->out_ptr[LSM_OUT_DEBUG_STAMPS];
+  P.diag = 0;
+#ifdef LSM_STAMPS
+  if (const char* v = getenv("LSM_DIAG")) P.diag = atoi(v);
+#endif
   P.pairs = e->pairs;
 }
 
