@@ -68,7 +68,7 @@ def _cpu_worker(k):
     return time.perf_counter() - t0
 
 
-def cpu_baseline(args, vt, tt, ep, cores, envs_per_worker=4, steps=250):
+def cpu_baseline(args, vt, tt, ep, cores, envs_per_worker=4, steps=500):
     _CPU_CTX.update(args=args, vt=vt, tt=tt, ep=ep, envs_per_worker=envs_per_worker, steps=steps)
     ctx = mp.get_context("fork")
     with ctx.Pool(cores) as pool:

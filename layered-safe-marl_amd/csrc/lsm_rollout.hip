@@ -127,7 +127,7 @@ struct KParams {
   double ttr_max;
   uint32_t m_E, m_EE, m_EF, m_F, m_EF4;  // ceil(2^32 / d) for exact small-numerator division
   unsigned long long* stamps;     // LSM_OUT_DEBUG_STAMPS (diagnostic builds only)
-  int diag;                       // diagnostic builds: bit 0 = skip adj/node stores (LSM_DIAG)
+  int diag;                       // diagnostic builds: bit 0 skip adj/node stores, bit 1 skip filter (LSM_DIAG)
   uint32_t lds_env_bytes;         // LDS bytes per env (envs per wave > 1: consecutive blocks)
   const uint16_t* pairs;          // strict upper-triangle entity pairs (a | b << 8)
   TableDev val, ttr;
@@ -1384,7 +1384,11 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams* __restrict__
   STAMP(2);
 
   // ---- 3. safety filter ---------------------------------------------------------------
+#ifdef LSM_STAMPS
+  const bool filter_on = S.cur[C_FILT] != 0.0 && !(P.diag & 2);   // diag bit 1: filter skipped
+#else
   const bool filter_on = S.cur[C_FILT] != 0.0;
+#endif
   if (filter_on) {
     const int npairs = N * N;
     for (int p = lane; p < npairs; p += LPE) {
