@@ -1117,13 +1117,15 @@ __device__ __forceinline__ void emit_graph(const KParams& P, Lds& S, int env) {
 // cached_dist_mag (core.py:514-543): float32 thresholded copy for the adjacency
 // (adj = d * (d < range) * (d > 0), navigation_graph_safe.py:991-992) + float64 agent block.
 template <int LPE, int NT>
-__device__ __forceinline__ void compute_dist(const KParams& P, Lds& S) {
+__device__ __forceinline__ void compute_dist(const KParams& P, Lds& S, const uint32_t* prw = nullptr) {
   const int lane = threadIdx.x & (LPE - 1);
   constexpr int DYN = 0;
   LSM_DIMS;
   const int npair = E * (E - 1) / 2;
+#pragma unroll
   for (int t = lane; t < npair; t += LPE) {
-    const uint32_t pr = gptr(P.pairs)[t];
+    // specialised kernels preload this lane's pair words with the record (prw)
+    const uint32_t pr = (NT && prw) ? prw[(t - lane) / LPE] : (uint32_t)gptr(P.pairs)[t];
     const int a = (int)(pr & 0xffu), b = (int)(pr >> 8);
     const double xa = a < N ? S.ps[a] : S.lm[a - N];
     const double ya = a < N ? S.ps[N + a] : S.lm[NL + a - N];
@@ -1335,6 +1337,17 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams* __restrict__
       for (int q = 1; q < 25; ++q) if (a[q] > best) { best = a[q]; ai = q; }
     }
   }
+  // this lane's E x E pair words (compute_dist), loaded in the same round trip as the record
+  constexpr bool PRE = NT != 0 && NT <= 8;   // <= 5 registers per lane
+  constexpr int NPI = PRE ? ((NT * 3) * (NT * 3 - 1) / 2 + LPE - 1) / LPE : 1;
+  uint32_t prw[NPI];
+  if (PRE) {
+#pragma unroll
+    for (int k = 0; k < NPI; ++k) {
+      const int t = lane + k * LPE;
+      prw[k] = gptr(P.pairs)[t < E * (E - 1) / 2 ? t : 0];
+    }
+  }
   rec_copy<LPE>((const GAS f32x4*)gptr(P.s.rec) + (size_t)env * P.s.rec_stride16, (f32x4*)lbase, P.s.rec16);
   __syncthreads();
   if (lane < N) {
@@ -1476,7 +1489,7 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams* __restrict__
   STAMP(5);
 
   // ---- 5. distances, min relative distance ---------------------------------------------
-  compute_dist<LPE, NT>(P, S);
+  compute_dist<LPE, NT>(P, S, PRE ? prw : nullptr);
   if (lane < N) {
     const int i = lane;
     double m = INFINITY;
