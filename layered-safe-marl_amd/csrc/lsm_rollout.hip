@@ -811,85 +811,76 @@ __device__ __forceinline__ void filter_ego(const KParams& P, Lds& S, int i, uint
 // Outputs: per-ego node features + adjacency with the sequential snapshot rule.
 // ego i sees agent j "post" (after its reward update) iff j <= i.
 // ----------------------------------------------------------------------------------
+// Airtaxi node features (utils.py:139-200, relative to the ego frame). Headings enter only
+// through sin / cos, so the per-agent trig table built once per emission (trig_table_at:
+// [0] cos th, [1] sin th, [2] vx, [3] vy unfrozen, per agent) and the cached landmark
+// sin / cos replace the per-(ego, entity) sin / cos of differences by the angle-difference
+// identities (fp32 outputs; ulp-level vs sin(a - b) in float64).
 template <int DYN, int NT>
 __device__ __forceinline__ void node_features(const KParams& P, const Lds& S, int e, int k, float* f) {
   LSM_DIMS;
+  const double* tc = S.feat;            // cos th [N]
+  const double* ts = S.feat + N;        // sin th [N]
+  const double* tvx = S.feat + 2 * N;   // unfrozen velocity [N]
+  const double* tvy = S.feat + 3 * N;
   const double pex = S.ps[e], pey = S.ps[N + e];
-  double vex, vey;
-  agent_vel<DYN>(S, N, e, true, vex, vey);
-  if (DYN == 0) {
-    if (k < N) {
-      const bool post = k <= e;
-      double vkx, vky;
-      agent_vel<DYN>(S, N, k, post, vkx, vky);
-      const int gi = goal_index(post ? S.rpost[k] : S.rpre[k], k, N, NL);
-      f[0] = (float)(S.ps[k] - pex);
-      f[1] = (float)(S.ps[N + k] - pey);
-      f[2] = (float)(vkx - vex);
-      f[3] = (float)(vky - vey);
-      f[4] = (float)(S.lm[gi] - pex);
-      f[5] = (float)(S.lm[NL + gi] - pey);
-      f[6] = (float)S.lmsc[gi];
-      f[7] = (float)S.lmsc[NL + gi];
-      f[8] = (float)S.lm[3 * NL + gi];
-      f[9] = 0.0f;
-    } else {
-      const int l = k - N;
-      const double rx = S.lm[l] - pex, ry = S.lm[NL + l] - pey;
-      f[0] = (float)rx;
-      f[1] = (float)ry;
-      f[2] = (float)(-vex);
-      f[3] = (float)(-vey);
-      f[4] = (float)rx;
-      f[5] = (float)ry;
-      f[6] = (float)S.lmsc[l];
-      f[7] = (float)S.lmsc[NL + l];
-      f[8] = (float)S.lm[3 * NL + l];
-      f[9] = 1.0f;
-    }
+  const double c = tc[e], s = ts[e];
+  const bool efz = S.dpost[e] != 0;     // the ego is seen after its own update
+  const double vex = efz ? 0.0 : tvx[e], vey = efz ? 0.0 : tvy[e];
+  if (k < N) {
+    const bool post = k <= e;
+    const bool kfz = post && S.dpost[k];
+    const double vkx = kfz ? 0.0 : tvx[k], vky = kfz ? 0.0 : tvy[k];
+    const int gi = goal_index(post ? S.rpost[k] : S.rpre[k], k, N, NL);
+    double rx, ry, gx, gy;
+    blas_rot(c, s, S.ps[k] - pex, S.ps[N + k] - pey, rx, ry);
+    const double rs = blas_norm2(vkx - vex, vky - vey);
+    blas_rot(c, s, S.lm[gi] - pex, S.lm[NL + gi] - pey, gx, gy);
+    const double sg = S.lmsc[gi], cg = S.lmsc[NL + gi];
+    f[0] = (float)rx;
+    f[1] = (float)ry;
+    f[2] = (float)rs;
+    f[3] = (float)(ts[k] * c - tc[k] * s);   // sin(th_k - th_e)
+    f[4] = (float)(tc[k] * c + ts[k] * s);   // cos(th_k - th_e)
+    f[5] = (float)gx;
+    f[6] = (float)gy;
+    f[7] = (float)(sg * c - cg * s);
+    f[8] = (float)(cg * c + sg * s);
+    f[9] = (float)S.lm[3 * NL + gi];
+    f[10] = 0.0f;
   } else {
-    const double th = S.ps[2 * N + e];
-    const double c = cos(th), s = sin(th);
-    if (k < N) {
-      const bool post = k <= e;
-      double vkx, vky;
-      agent_vel<DYN>(S, N, k, post, vkx, vky);
-      const int gi = goal_index(post ? S.rpost[k] : S.rpre[k], k, N, NL);
-      double rx, ry, gx, gy;
-      blas_rot(c, s, S.ps[k] - pex, S.ps[N + k] - pey, rx, ry);
-      const double rh = S.ps[2 * N + k] - th;
-      const double rs = blas_norm2(vkx - vex, vky - vey);
-      blas_rot(c, s, S.lm[gi] - pex, S.lm[NL + gi] - pey, gx, gy);
-      const double rgh = S.lm[2 * NL + gi] - th;
-      f[0] = (float)rx;
-      f[1] = (float)ry;
-      f[2] = (float)rs;
-      f[3] = (float)sin(rh);
-      f[4] = (float)cos(rh);
-      f[5] = (float)gx;
-      f[6] = (float)gy;
-      f[7] = (float)sin(rgh);
-      f[8] = (float)cos(rgh);
-      f[9] = (float)S.lm[3 * NL + gi];
-      f[10] = 0.0f;
-    } else {
-      const int l = k - N;
-      double rx, ry;
-      blas_rot(c, s, S.lm[l] - pex, S.lm[NL + l] - pey, rx, ry);
-      const double rh = S.lm[2 * NL + l] - th;
-      const float sn = (float)sin(rh), cs = (float)cos(rh);
-      f[0] = (float)rx;
-      f[1] = (float)ry;
-      f[2] = (float)agent_speed<DYN>(S, N, e, true);
-      f[3] = sn;
-      f[4] = cs;
-      f[5] = (float)rx;
-      f[6] = (float)ry;
-      f[7] = sn;
-      f[8] = cs;
-      f[9] = (float)S.lm[3 * NL + l];
-      f[10] = 1.0f;
-    }
+    const int l = k - N;
+    double rx, ry;
+    blas_rot(c, s, S.lm[l] - pex, S.lm[NL + l] - pey, rx, ry);
+    const double sl = S.lmsc[l], cl = S.lmsc[NL + l];
+    const float sn = (float)(sl * c - cl * s), cs = (float)(cl * c + sl * s);
+    f[0] = (float)rx;
+    f[1] = (float)ry;
+    f[2] = (float)(efz ? 0.0 : S.ps[3 * N + e]);
+    f[3] = sn;
+    f[4] = cs;
+    f[5] = (float)rx;
+    f[6] = (float)ry;
+    f[7] = sn;
+    f[8] = cs;
+    f[9] = (float)S.lm[3 * NL + l];
+    f[10] = 1.0f;
+  }
+}
+
+// per-agent heading trig + unfrozen velocity for node_features<1> (in the DI row area of U2)
+template <int LPE, int NT>
+__device__ __forceinline__ void trig_table_at(const KParams& P, Lds& S) {
+  const int lane = threadIdx.x & (LPE - 1);
+  constexpr int DYN = 1;
+  LSM_DIMS;
+  for (int j = lane; j < N; j += LPE) {
+    const double th = S.ps[2 * N + j], sp = S.ps[3 * N + j];
+    const double c = cos(th), sn = sin(th);
+    S.feat[j] = c;
+    S.feat[N + j] = sn;
+    S.feat[2 * N + j] = sp * c;
+    S.feat[3 * N + j] = sp * sn;
   }
 }
 
@@ -951,7 +942,7 @@ template <int DYN, int LPE, int NT>
 __device__ __forceinline__ void emit_graph(const KParams& P, Lds& S, int env) {
   const int lane = threadIdx.x & (LPE - 1);
   LSM_DIMS;
-  if (DYN == 0) build_rows_di<LPE, NT>(P, S);
+  if (DYN == 0) build_rows_di<LPE, NT>(P, S); else trig_table_at<LPE, NT>(P, S);
   __syncthreads();
   // No agent changed done / reached status this step (the common case): every ego then has
   // the same disconnect mask and the same (pre == post) entity rows, so each lane computes
