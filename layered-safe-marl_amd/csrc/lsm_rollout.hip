@@ -125,7 +125,7 @@ struct KParams {
   double at_vmax, at_vmin, at_amax, at_amin, at_wmax, at_thr_amax, at_thr_amin;
   float at_box_w, at_box_amax, at_box_amin;  // float32 box corners (jnp)
   double ttr_max;
-  uint32_t m_E, m_EE, m_EF, m_F, m_EF4;  // ceil(2^32 / d) for exact small-numerator division
+  uint32_t m_E, m_EE, m_EF, m_F, m_EF4, m_NL;  // ceil(2^32 / d) for exact small-numerator division
   unsigned long long* stamps;     // LSM_OUT_DEBUG_STAMPS (diagnostic builds only)
   int diag;                       // diagnostic builds: bit 0 skip adj/node stores, bit 1 skip filter (LSM_DIAG)
   uint32_t lds_env_bytes;         // LDS bytes per env (envs per wave > 1: consecutive blocks)
@@ -165,6 +165,7 @@ struct Lds {
   double* cur;       // [NCUR]
   double* lm;        // [6][NL] x, y, heading, speed, sin, cos
   double* lmsc;      // = lm + 4 NL
+  float* lmd;        // [NL(NL-1)/2] thresholded landmark-landmark distances (per episode)
   // ---- step scratch ----
   int32_t* dpre;     // [N] done before reward update
   int32_t* rpre;     // [N] reached_goal before
@@ -173,6 +174,7 @@ struct Lds {
   double* wold;      // [2][N] dists_to_goal / times_required before this step's info
   double* wnew;      // [2][N] after
   uint64_t* emask;   // [N] bit r: entity r disconnected for ego e (snapshot rule)
+  double* ecs;       // [2][N] cos / sin of the heading at step start (airtaxi filter frame)
   // U1
   float* fval;       // [E][E] d if 0 < d < range else 0 (float32, unmasked)
   double* aa;        // [N][N] float64 agent-agent distances (episode stats)
@@ -256,10 +258,11 @@ __host__ __device__ inline LdsPlan lds_plan(int N, int NL, int E, int F) {
   put(8 * N); put(8 * N); put(8 * N); put(8 * N);
   put(4 * N); put(4 * N); put(4 * N); put(4 * N); put(4);
   p.hot = o;
-  put(8 * NCUR); put(8 * 6 * NL);
+  put(8 * NCUR); put(8 * 6 * NL); put(4 * (NL * (NL - 1) / 2));
   p.rec = o;
   // scratch
   put(4 * N); put(4 * N); put(8 * 2 * N); put(8 * 2 * N); put(8 * 2 * N); put(8 * 2 * N); put(8 * N);
+  put(F == 10 ? 0 : 8 * 2 * N);
   // U1
   const size_t u1 = o;
   size_t a = align16(4 * E * E), a2 = a + align16(8 * N * N), b = a2 + align16(8 * N * N);
@@ -273,11 +276,14 @@ __host__ __device__ inline LdsPlan lds_plan(int N, int NL, int E, int F) {
   // U2
   const size_t u2 = o;
   size_t f1 = align16(8 * N * N), f2 = f1 + align16(4 * N * N), f3 = f2 + align16(N * N);
-  size_t g1 = align16(8 * (2 * N + NL) * F), g2 = g1 + align16(8 * N * F);
+  // DI entity rows + ego offsets; airtaxi: the [4][N] heading trig table (feat) only
+  size_t g1 = F == 10 ? align16(8 * (2 * N + NL) * F) : align16(8 * 4 * N);
+  size_t g2 = g1 + (F == 10 ? align16(8 * N * F) : 0);
   p.off[k++] = u2; p.off[k++] = u2 + f1; p.off[k++] = u2 + f2;
   p.off[k++] = u2; p.off[k++] = u2 + g1; p.off[k++] = u1;   // stage aliases U1 (adj emitted first)
   size_t m = f3 > g2 ? f3 : g2;
-  m = m > (size_t)(8 * 2 * 64) ? m : (size_t)(8 * 2 * 64);   // magnetic partial sums (filter off)
+  if (F == 10) m = m > (size_t)(8 * 2 * 64) ? m : (size_t)(8 * 2 * 64);   // magnetic partials (DI, filter off)
+  m = m > (size_t)(8 * 16 * N) ? m : (size_t)(8 * 16 * N);                  // info row staging
   o = u2 + m;
   p.bytes = o;
   return p;
@@ -302,6 +308,7 @@ __device__ __forceinline__ Lds carve(unsigned char* base, int N, int NL, int E, 
   L.cur = (double*)(base + p.off[k++]);
   L.lm = (double*)(base + p.off[k++]);
   L.lmsc = L.lm + 4 * NL;
+  L.lmd = (float*)(base + p.off[k++]);
   L.dpre = (int32_t*)(base + p.off[k++]);
   L.rpre = (int32_t*)(base + p.off[k++]);
   L.raw = (double*)(base + p.off[k++]);
@@ -309,6 +316,7 @@ __device__ __forceinline__ Lds carve(unsigned char* base, int N, int NL, int E, 
   L.wold = (double*)(base + p.off[k++]);
   L.wnew = (double*)(base + p.off[k++]);
   L.emask = (uint64_t*)(base + p.off[k++]);
+  L.ecs = (double*)(base + p.off[k++]);
   L.fval = (float*)(base + p.off[k++]);
   L.aa = (double*)(base + p.off[k++]);
   L.aa2 = (double*)(base + p.off[k++]);
@@ -652,12 +660,13 @@ __device__ __forceinline__ void rel_state(const Lds& S, int N, int e, int o, dou
   if (DYN == 0) {
     rel[0] = ex - ox; rel[1] = ey - oy; rel[2] = e2 - o2; rel[3] = e3 - o3;
   } else {
-    const double d = sqrt((ox - ex) * (ox - ex) + (oy - ey) * (oy - ey));
-    const double rh = o2 - e2;
-    const double ang = atan2(oy - ey, ox - ex);
-    rel[0] = d * cos(ang - e2);
-    rel[1] = d * sin(ang - e2);
-    rel[2] = rh;
+    // |d| cos / sin(atan2(dy, dx) - th_e) (safety_filter.py:277-284) as the rotation of d
+    // into the ego frame (ulp-level in float64; the grid lookup rounds to float32)
+    const double c = S.ecs[e], sn = S.ecs[N + e];
+    const double dx = ox - ex, dy = oy - ey;
+    rel[0] = dx * c + dy * sn;
+    rel[1] = dy * c - dx * sn;
+    rel[2] = o2 - e2;
     rel[3] = e3;
     rel[4] = o3;
   }
@@ -1107,16 +1116,22 @@ __device__ __forceinline__ void emit_graph(const KParams& P, Lds& S, int env) {
 
 // cached_dist_mag (core.py:514-543): float32 thresholded copy for the adjacency
 // (adj = d * (d < range) * (d > 0), navigation_graph_safe.py:991-992) + float64 agent block.
+// cached_dist_mag (core.py:514-543): float32 thresholded copy for the adjacency
+// (adj = d * (d < range) * (d > 0), navigation_graph_safe.py:991-992) + float64 agent block.
+// Landmarks do not move within an episode: their pairwise block is computed at the reset
+// (`full`) into the record (lmd) and copied in afterwards.
 template <int LPE, int NT>
-__device__ __forceinline__ void compute_dist(const KParams& P, Lds& S, const uint32_t* prw = nullptr) {
+__device__ __forceinline__ void compute_dist(const KParams& P, Lds& S, const uint32_t* prw = nullptr,
+                                             bool full = false) {
   const int lane = threadIdx.x & (LPE - 1);
   constexpr int DYN = 0;
   LSM_DIMS;
-  const int npair = E * (E - 1) / 2;
+  const int nmov = N * (N - 1) / 2 + N * NL;   // pairs with an agent (pair table classes 0, 1)
+  const int npair = full ? E * (E - 1) / 2 : nmov;
 #pragma unroll
   for (int t = lane; t < npair; t += LPE) {
     // specialised kernels preload this lane's pair words with the record (prw)
-    const uint32_t pr = (NT && prw) ? prw[(t - lane) / LPE] : (uint32_t)gptr(P.pairs)[t];
+    const uint32_t pr = (NT && prw && t < nmov) ? prw[(t - lane) / LPE] : (uint32_t)gptr(P.pairs)[t];
     const int a = (int)(pr & 0xffu), b = (int)(pr >> 8);
     const double xa = a < N ? S.ps[a] : S.lm[a - N];
     const double ya = a < N ? S.ps[N + a] : S.lm[NL + a - N];
@@ -1127,12 +1142,22 @@ __device__ __forceinline__ void compute_dist(const KParams& P, Lds& S, const uin
     const float fv = (d < P.coord_range && d > 0) ? (float)d : 0.0f;
     S.fval[a * E + b] = fv;
     S.fval[b * E + a] = fv;
+    if (t >= nmov) S.lmd[t - nmov] = fv;
     if (b < N) {
       const double d2 = blas_norm2(dx, dy);
       S.aa[a * N + b] = d;
       S.aa[b * N + a] = d;
       S.aa2[a * N + b] = d2;
       S.aa2[b * N + a] = d2;
+    }
+  }
+  if (!full) {
+    // landmark block from the episode cache: u = (la, lb) over NL x NL (diagonal -> 0 below)
+    for (int u = lane; u < NL * NL; u += LPE) {
+      const int la = qdiv<NT>(u, NL, P.m_NL), lb = u - la * NL;
+      if (la == lb) continue;
+      const int lo = la < lb ? la : lb, hi = la < lb ? lb : la;
+      S.fval[(N + la) * E + N + lb] = S.lmd[lo * (2 * NL - lo - 1) / 2 + (hi - lo - 1)];
     }
   }
   for (int k = lane; k < E; k += LPE) {
@@ -1250,7 +1275,7 @@ __device__ __forceinline__ void reset_env(const KParams& P, Lds& S, int env, con
   }
   if (lane == 0) S.step[0] = 0;
   __syncthreads();   // MT words read out of U1 before compute_dist overwrites it
-  compute_dist<LPE, NT>(P, S);
+  compute_dist<LPE, NT>(P, S, nullptr, true);
   if (lane < N) write_obs<DYN, NT>(P, S, env, lane);
   emit_graph<DYN, LPE, NT>(P, S, env);
 }
@@ -1330,13 +1355,13 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams* __restrict__
   }
   // this lane's E x E pair words (compute_dist), loaded in the same round trip as the record
   constexpr bool PRE = NT != 0 && NT <= 8;   // <= 5 registers per lane
-  constexpr int NPI = PRE ? ((NT * 3) * (NT * 3 - 1) / 2 + LPE - 1) / LPE : 1;
+  constexpr int NPI = PRE ? ((NT * (NT - 1) / 2 + NT * 2 * NT) + LPE - 1) / LPE : 1;
   uint32_t prw[NPI];
   if (PRE) {
 #pragma unroll
     for (int k = 0; k < NPI; ++k) {
       const int t = lane + k * LPE;
-      prw[k] = gptr(P.pairs)[t < E * (E - 1) / 2 ? t : 0];
+      prw[k] = gptr(P.pairs)[t < E * (E - 1) / 2 ? t : 0];   // classes 0, 1 come first
     }
   }
   rec_copy<LPE>((const GAS f32x4*)gptr(P.s.rec) + (size_t)env * P.s.rec_stride16, (f32x4*)lbase, P.s.rec16);
@@ -1344,6 +1369,10 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams* __restrict__
   if (lane < N) {
     S.dpre[lane] = S.dpost[lane];
     S.rpre[lane] = S.rpost[lane];
+    if (DYN == 1) {
+      S.ecs[lane] = cos(S.ps[2 * N + lane]);
+      S.ecs[N + lane] = sin(S.ps[2 * N + lane]);
+    }
   }
   const int cstep = S.step[0] + 1;
   __syncthreads();
@@ -1812,6 +1841,7 @@ static void fill_params(const lsm_env* e, KParams& P) {
   P.m_EF = magic(e->E * e->F);
   P.m_F = magic(e->F);
   P.m_EF4 = magic(e->E * e->F / 4);
+  P.m_NL = magic(e->NL);
   P.ttr_max = e->ttr_max;
   P.val = e->val;
   P.ttr = e->ttr;

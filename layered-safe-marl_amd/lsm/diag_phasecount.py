@@ -50,7 +50,7 @@ def run(config):
     env.close()
 
 
-def reduce(d):
+def reduce(d, config=3):
     import statistics
     from .pmc import _rows
     per = {}
@@ -73,7 +73,9 @@ def reduce(d):
     from .diag_stamps import PHASES
     print("%-14s" % "phase" + "".join("%16s" % n for n in names) + "   (per wave)")
     prev = {n: 0.0 for n in names}
-    nw = 4096.0
+    sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+    import bench
+    nw = float(bench.CONFIGS[config]["envs"])
     for k in STOPS:
         label = "start" if k == 0 else (PHASES[k - 1] if k <= len(PHASES) else "store")
         print("%-14s" % label + "".join("%16.0f" % ((cum[k][n] - prev[n]) / nw) for n in names))
@@ -86,6 +88,6 @@ if __name__ == "__main__":
     ap.add_argument("--reduce", default=None)
     a = ap.parse_args()
     if a.reduce:
-        reduce(a.reduce)
+        reduce(a.reduce, a.config)
     else:
         run(a.config)

@@ -7,8 +7,9 @@ path, per env:
   written back up to the curriculum block: agent state 4N f64, episode stats 6N f64,
   info accumulators 4N f64, travel distance / goal_min_time / min relative distance /
   action diff N f64 each, done / reached / safety flag / deconflicting index N i32
-  each, step counter i32 (every field 16-B aligned) | curriculum block 12 f64 and
-  landmarks 6NL f64 (read only; written back only at a reset);
+  each, step counter i32 (every field 16-B aligned) | curriculum block 12 f64,
+  landmarks 6NL f64 and the landmark-pair distance cache NL(NL-1)/2 f32 (read only;
+  written back only at a reset);
 * actions: N i32 read;
 * outputs written: obs N*OBS f32, node_obs N*E*F f32, adj N*E*E f32, reward N f32,
   done N u8, reset flag 1 u8, info N*16 f64, state copy 4N f64.
@@ -28,7 +29,7 @@ def step_bytes(N: int, L: int = 2, dynamics: str = "double_integrator", filter_o
     OBS = 7 if di else 6
     a16 = lambda x: (x + 15) // 16 * 16
     hot = (a16(8 * 4 * N) + a16(8 * 6 * N) + a16(8 * 4 * N) + 4 * a16(8 * N) + 4 * a16(4 * N) + 16)
-    rec = hot + a16(8 * 12) + a16(8 * 6 * NL)
+    rec = hot + a16(8 * 12) + a16(8 * 6 * NL) + a16(4 * (NL * (NL - 1) // 2))
     state_r = rec + N * 4
     state_w = hot
     outputs = N * OBS * 4 + N * E * F * 4 + N * E * E * 4 + N * 4 + N + 1 + N * 16 * 8 + 4 * N * 8
