@@ -947,8 +947,50 @@ __device__ __forceinline__ void build_rows_di(const KParams& P, Lds& S) {
 // pair by one lane, staged in LDS, and copied out as contiguous float4 when the env block is
 // 16-byte aligned; the adjacency is a masked select over the thresholded distance table,
 // one float4 (4 columns of one row) per lane-iteration when E % 4 == 0.
+// Adjacency of egos [e0, e1) when every ego shares the disconnect mask m (E % 4 == 0): each
+// lane owns fixed float4 column groups of the E x E table, masks them once and stores them
+// for every ego of the range.
+template <int LPE, int NT>
+__device__ __forceinline__ void emit_adj_uniform(const KParams& P, const Lds& S, int env, uint64_t m, int e0,
+                                                 int e1) {
+  const int lane = threadIdx.x & (LPE - 1);
+  constexpr int DYN = 0;
+  LSM_DIMS;
+  const int EE = E * E;
+  GAS float* adj_out = gptr(P.o.adj) + (size_t)env * N * EE;
+  const int Q = EE / 4, last = Q - 1;
+  for (int t0 = lane; t0 < Q; t0 += 4 * LPE) {
+    int u[4];
+    float4 w[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int t = t0 + j * LPE;
+      u[j] = 4 * (t < last ? t : last);
+      const int r = qdiv<NT>(u[j], E, P.m_E);
+      const int c = u[j] - r * E;
+      w[j] = *(const float4*)(S.fval + u[j]);
+      const uint32_t bits = ((m >> r) & 1ull) ? 0xfu : ((uint32_t)(m >> c) & 0xfu);
+      if (bits & 1u) w[j].x = 0.f;
+      if (bits & 2u) w[j].y = 0.f;
+      if (bits & 4u) w[j].z = 0.f;
+      if (bits & 8u) w[j].w = 0.f;
+    }
+#ifdef LSM_STAMPS
+    if (P.diag & 1) continue;
+#endif
+    for (int e = e0; e < e1; ++e) {
+      GAS float* dst = adj_out + (size_t)e * EE;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (t0 + j * LPE <= last) st_stream(dst + u[j], w[j]);
+    }
+  }
+}
+
+// `adj_done`: the uniform adjacency was already stored (speculatively, in chunks during the
+// step); it is rewritten here only if an agent changed status.
 template <int DYN, int LPE, int NT>
-__device__ __forceinline__ void emit_graph(const KParams& P, Lds& S, int env) {
+__device__ __forceinline__ void emit_graph(const KParams& P, Lds& S, int env, bool adj_done = false) {
   const int lane = threadIdx.x & (LPE - 1);
   LSM_DIMS;
   if (DYN == 0) build_rows_di<LPE, NT>(P, S); else trig_table_at<LPE, NT>(P, S);
@@ -961,34 +1003,7 @@ __device__ __forceinline__ void emit_graph(const KParams& P, Lds& S, int env) {
   const int EE = E * E, atot = N * EE;
   GAS float* adj_out = gptr(P.o.adj) + (size_t)env * atot;
   if ((E & 3) == 0 && uni) {
-    const int Q = EE / 4, last = Q - 1;
-    const uint64_t m = S.emask[0];
-    for (int t0 = lane; t0 < Q; t0 += 4 * LPE) {
-      int u[4];
-      float4 w[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int t = t0 + j * LPE;
-        u[j] = 4 * (t < last ? t : last);
-        const int r = qdiv<NT>(u[j], E, P.m_E);
-        const int c = u[j] - r * E;
-        w[j] = *(const float4*)(S.fval + u[j]);
-        const uint32_t bits = ((m >> r) & 1ull) ? 0xfu : ((uint32_t)(m >> c) & 0xfu);
-        if (bits & 1u) w[j].x = 0.f;
-        if (bits & 2u) w[j].y = 0.f;
-        if (bits & 4u) w[j].z = 0.f;
-        if (bits & 8u) w[j].w = 0.f;
-      }
-#ifdef LSM_STAMPS
-      if (P.diag & 1) continue;
-#endif
-      for (int e = 0; e < N; ++e) {
-        GAS float* dst = adj_out + (size_t)e * EE;
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          if (t0 + j * LPE <= last) st_stream(dst + u[j], w[j]);
-      }
-    }
+    if (!adj_done) emit_adj_uniform<LPE, NT>(P, S, env, S.emask[0], 0, N);
   } else if ((E & 3) == 0) {
     // Each lane owns fixed float4 column groups u of the E x E table (loaded from LDS once)
     // and writes them for every ego: per ego only the mask word is read.
@@ -1522,6 +1537,13 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams* __restrict__
     }
     S.minrel[i] = m;
   }
+  // Speculative adjacency: unless an agent changes done / reached status below (rare), every
+  // ego's mask is the pre-update mask, so the adjacency can be stored now, in four chunks of
+  // egos placed between the remaining phases: the stores drain while the wave computes
+  // instead of queueing behind each other at the end. A status change rewrites it at the end.
+  const bool chunked = (E & 3) == 0;
+  const uint64_t m_pre = chunked ? ego_mask(S, N, L, -1) : 0;
+  if (chunked) emit_adj_uniform<LPE, NT>(P, S, env, m_pre, 0, N / 4);
   STAMP(6);
 
   // ---- 6. obs, reward, goal/done update ---------------------------------------------------
@@ -1605,6 +1627,7 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams* __restrict__
   }
   __syncthreads();
   if (lane < N) S.emask[lane] = ego_mask(S, N, L, lane);
+  if (chunked) emit_adj_uniform<LPE, NT>(P, S, env, m_pre, N / 4, N / 2);
   STAMP(7);
 
   // ---- 7/8. info_callback numbers -----------------------------------------------------
@@ -1680,6 +1703,7 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams* __restrict__
   __syncthreads();
   rec_copy<LPE>((const f32x4*)S.dpair, (GAS f32x4*)(gptr(P.o.info) + (size_t)env * N * LSM_INFO_FIELDS),
                 N * LSM_INFO_FIELDS / 2);
+  if (chunked) emit_adj_uniform<LPE, NT>(P, S, env, m_pre, N / 2, 3 * N / 4);
   STAMP(8);
 
   // ---- episode stats (environment.py:1004-1022), dones ---------------------------------
@@ -1713,6 +1737,7 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams* __restrict__
     gptr(P.o.dones)[(size_t)env * N + i] = my_done ? 1 : 0;
   }
   const bool all_done = group_all<LPE>(my_done);
+  if (chunked && !(P.auto_reset && all_done)) emit_adj_uniform<LPE, NT>(P, S, env, m_pre, 3 * N / 4, N);
   __syncthreads();
   STAMP(9);
 
@@ -1726,7 +1751,7 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams* __restrict__
     store_state<DYN, LPE, NT>(P, S, lbase, env, true);
   } else {
     if (lane == 0) gptr(P.o.reset_flag)[env] = 0;
-    emit_graph<DYN, LPE, NT>(P, S, env);
+    emit_graph<DYN, LPE, NT>(P, S, env, chunked);
     __syncthreads();
     STAMP(10);
     store_state<DYN, LPE, NT>(P, S, lbase, env, false);
