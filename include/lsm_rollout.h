@@ -119,6 +119,13 @@ int lsm_reset(lsm_env* env, const lsm_curriculum* cur, void* hip_stream);
 int lsm_step(lsm_env* env, const void* actions_device, int32_t action_kind,
              const lsm_curriculum* cur_for_auto_reset, void* hip_stream);
 
+/* Overwrite the agent states ([N][4], the LSM_OUT_STATE layout) and, if non-null,
+ * reached_goal ([N]) of one env between calls -- what scripts do to `world.agents[i].state` /
+ * `scenario.reached_goal` between env.step calls (e.g. tests/golden/make_golden.py's injection,
+ * navigation_graph_safe.py:276-317 state fields). Synchronises `hip_stream` first. */
+int lsm_set_agent_state(lsm_env* env, int32_t env_index, const double* agent_state,
+                        const int32_t* reached, void* hip_stream);
+
 /* Shape helpers. */
 int32_t lsm_num_entities(const lsm_env* env);   /* E = N * (1 + L) */
 int32_t lsm_node_features(const lsm_env* env);  /* F */

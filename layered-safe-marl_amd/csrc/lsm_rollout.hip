@@ -161,7 +161,7 @@ struct Lds {
   int32_t* rpost;    // [N] reached_goal after (record: reached)
   int32_t* sfilt;    // [N]
   int32_t* decon;    // [N]
-  int32_t* step;     // [1] env.current_step
+  int32_t* step;     // [2] env.current_step; 1 = cached distances unmasked (state edited)
   double* cur;       // [NCUR]
   double* lm;        // [6][NL] x, y, heading, speed, sin, cos
   double* lmsc;      // = lm + 4 NL
@@ -256,7 +256,7 @@ __host__ __device__ inline LdsPlan lds_plan(int N, int NL, int E, int F) {
   // record
   put(8 * 4 * N); put(8 * NSTAT * N); put(8 * NWINFO * N);
   put(8 * N); put(8 * N); put(8 * N); put(8 * N);
-  put(4 * N); put(4 * N); put(4 * N); put(4 * N); put(4);
+  put(4 * N); put(4 * N); put(4 * N); put(4 * N); put(8);
   p.hot = o;
   put(8 * NCUR); put(8 * 6 * NL); put(4 * (NL * (NL - 1) / 2));
   p.rec = o;
@@ -1288,7 +1288,7 @@ __device__ __forceinline__ void reset_env(const KParams& P, Lds& S, int env, con
     S.pdist[k] = 0.0;
     S.gmt[k] = plain_norm2(S.ps[k] - S.lm[k], S.ps[N + k] - S.lm[NL + k]) / P.max_speed;
   }
-  if (lane == 0) S.step[0] = 0;
+  if (lane == 0) { S.step[0] = 0; S.step[1] = 0; }
   __syncthreads();   // MT words read out of U1 before compute_dist overwrites it
   compute_dist<LPE, NT>(P, S, nullptr, true);
   if (lane < N) write_obs<DYN, NT>(P, S, env, lane);
@@ -1403,7 +1403,9 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams* __restrict__
   // ---- 1. update_graph() at step start (previous state, final masks) --------------
   if (K.emit_edges) {
     GAS uint8_t* eo = gptr(P.o.edges) + (size_t)env * E * E;
-    const uint64_t m0 = ego_mask(S, N, L, N);
+    // the previous step's observation masked cached_dist_mag in place; after an edit of the
+    // state (lsm_set_agent_state = world.calculate_distances()) it is fresh
+    const uint64_t m0 = S.step[1] ? 0ull : ego_mask(S, N, L, N);
     for (int u = lane; u < E * E; u += LPE) {
       const int a = qdiv<NT>(u, E, P.m_E), b = u - a * E;
       double d = 0.0;
@@ -1742,7 +1744,7 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams* __restrict__
   STAMP(9);
 
   // ---- 9. graph outputs, or the auto-reset (whose outputs replace them) ---------------------
-  if (lane == 0) S.step[0] = cstep;
+  if (lane == 0) { S.step[0] = cstep; S.step[1] = 0; }
   if (P.auto_reset && all_done) {
     if (lane == 0) gptr(P.o.reset_flag)[env] = 1;
     reset_env<DYN, LPE, NT>(P, S, env, K.cur_new);
@@ -2146,6 +2148,27 @@ static int launch(lsm_env* e, KStep& L, hipStream_t st) {
     }
   }
   HIPCHK(e, hipGetLastError());
+  return 0;
+}
+
+int lsm_set_agent_state(lsm_env* e, int32_t env_index, const double* state, const int32_t* reached,
+                        void* stream) {
+  if (!e || !state) return 1;
+  if (env_index < 0 || env_index >= e->cfg.num_envs) return fail(e, "env_index out of range");
+  HIPCHK(e, hipStreamSynchronize((hipStream_t)stream));
+  const LdsPlan lp = lds_plan(e->N, e->NL, e->E, e->F);
+  std::vector<unsigned char> rec(lp.rec);
+  float4* dev = e->s.rec + (size_t)env_index * e->s.rec_stride16;
+  HIPCHK(e, hipMemcpy(rec.data(), dev, lp.rec, hipMemcpyDeviceToHost));
+  double* ps = (double*)(rec.data() + lp.off[0]);   // record field 0: agent state [4][N]
+  for (int i = 0; i < e->N; ++i)
+    for (int c = 0; c < 4; ++c) ps[c * e->N + i] = state[i * 4 + c];
+  if (reached) {
+    int32_t* rp = (int32_t*)(rec.data() + lp.off[8]);   // record field 8: reached_goal
+    for (int i = 0; i < e->N; ++i) rp[i] = reached[i];
+  }
+  ((int32_t*)(rec.data() + lp.off[11]))[1] = 1;   // step slot: distances recomputed, unmasked
+  HIPCHK(e, hipMemcpy(dev, rec.data(), lp.rec, hipMemcpyHostToDevice));
   return 0;
 }
 

@@ -26,7 +26,8 @@ INFO_FIELDS = ("individual_reward", "min_relative_distance", "Dist_to_goal", "Ti
 # Every symbol include/lsm_rollout.h declares (checked by tests/test_capi.py).
 EXPORTED = ("lsm_create", "lsm_destroy", "lsm_last_error", "lsm_set_value_table", "lsm_set_ttr_table",
             "lsm_bind_output", "lsm_output_bytes", "lsm_reset", "lsm_step", "lsm_num_entities",
-            "lsm_node_features", "lsm_obs_dim", "lsm_host_mt_uniforms", "lsm_host_scenario")
+            "lsm_node_features", "lsm_obs_dim", "lsm_host_mt_uniforms", "lsm_host_scenario",
+            "lsm_set_agent_state")
 
 
 class LsmConfig(C.Structure):
@@ -76,6 +77,7 @@ def load_library(path: str = LIB_PATH):
         "lsm_obs_dim": (I32, [P]),
         "lsm_host_mt_uniforms": (I32, [U32, I32, D, D, P]),
         "lsm_host_scenario": (I32, [C.POINTER(LsmConfig), C.POINTER(LsmCurriculum), U32, P, P]),
+        "lsm_set_agent_state": (I32, [P, I32, P, P, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

@@ -250,6 +250,14 @@ class GpuGraphVecEnv:
             out.append(lst)
         return tuple(out)
 
+    def set_agent_state(self, env_index: int, agent_state, reached=None):
+        """Overwrite one env's agent states ([N][4]) and optionally reached_goal ([N])."""
+        st = np.ascontiguousarray(agent_state, dtype=np.float64).reshape(self.N, 4)
+        rp = None if reached is None else np.ascontiguousarray(reached, dtype=np.int32).reshape(self.N)
+        capi.check(self.lib.lsm_set_agent_state(
+            self.h, int(env_index), st.ctypes.data_as(C.c_void_p),
+            None if rp is None else rp.ctypes.data_as(C.c_void_p), self._stream()), self.h)
+
     def state(self):
         """Agent states [n, N, 4] (float64) after the last call (positions/velocities)."""
         return self.t_state
