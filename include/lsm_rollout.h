@@ -63,6 +63,7 @@ enum {
   LSM_INFO_DISTANCE_VARIANCE, LSM_INFO_DISTS_TRAVELED, LSM_INFO_TIME_MEAN, LSM_INFO_TIME_STDDEV,
   LSM_INFO_MIN_TIME_TO_GOAL, LSM_INFO_SAFETY_FILTERED, LSM_INFO_SAFETY_VIOLATED,
   LSM_INFO_DECONFLICTING_INDEX, LSM_INFO_ACTION_DIFF, LSM_INFO_REACHED_GOAL,
+  LSM_INFO_POSITION_X, LSM_INFO_POSITION_Y, /* 'position' = agent.state.p_pos at info time */
   LSM_INFO_FIELDS
 };
 

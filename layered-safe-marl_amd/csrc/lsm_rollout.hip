@@ -283,7 +283,7 @@ __host__ __device__ inline LdsPlan lds_plan(int N, int NL, int E, int F) {
   p.off[k++] = u2; p.off[k++] = u2 + g1; p.off[k++] = u1;   // stage aliases U1 (adj emitted first)
   size_t m = f3 > g2 ? f3 : g2;
   if (F == 10) m = m > (size_t)(8 * 2 * 64) ? m : (size_t)(8 * 2 * 64);   // magnetic partials (DI, filter off)
-  m = m > (size_t)(8 * 16 * N) ? m : (size_t)(8 * 16 * N);                  // info row staging
+  m = m > (size_t)(8 * LSM_INFO_FIELDS * N) ? m : (size_t)(8 * LSM_INFO_FIELDS * N);   // info rows
   o = u2 + m;
   p.bytes = o;
   return p;
@@ -1701,6 +1701,8 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams* __restrict__
     inf[LSM_INFO_DECONFLICTING_INDEX] = (double)S.decon[i];
     inf[LSM_INFO_ACTION_DIFF] = S.adiff[i];
     inf[LSM_INFO_REACHED_GOAL] = (double)S.rpost[i];
+    inf[LSM_INFO_POSITION_X] = S.ps[i];
+    inf[LSM_INFO_POSITION_Y] = S.ps[N + i];
   }
   __syncthreads();
   rec_copy<LPE>((const f32x4*)S.dpair, (GAS f32x4*)(gptr(P.o.info) + (size_t)env * N * LSM_INFO_FIELDS),

@@ -21,7 +21,7 @@ NUM_OUT = 11
 INFO_FIELDS = ("individual_reward", "min_relative_distance", "Dist_to_goal", "Time_req_to_goal",
                "Num_agent_collisions", "Distance_mean", "Distance_variance", "Dists_traveled",
                "Time_mean", "Time_stddev", "Min_time_to_goal", "Safety filtered", "Safety violated",
-               "deconflicting_agent_index", "action_diff", "reached_goal")
+               "deconflicting_agent_index", "action_diff", "reached_goal", "position_x", "position_y")
 
 # Every symbol include/lsm_rollout.h declares (checked by tests/test_capi.py).
 EXPORTED = ("lsm_create", "lsm_destroy", "lsm_last_error", "lsm_set_value_table", "lsm_set_ttr_table",

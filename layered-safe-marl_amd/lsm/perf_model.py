@@ -12,7 +12,7 @@ path, per env:
   written back only at a reset);
 * actions: N i32 read;
 * outputs written: obs N*OBS f32, node_obs N*E*F f32, adj N*E*E f32, reward N f32,
-  done N u8, reset flag 1 u8, info N*16 f64, state copy 4N f64.
+  done N u8, reset flag 1 u8, info N*18 f64, state copy 4N f64.
 
 HJ-table gathers (16 or 32 corners per pair) are served from the 256 MiB
 Infinity Cache / L2 for the 125 MB full-size table and are reported separately
@@ -32,7 +32,7 @@ def step_bytes(N: int, L: int = 2, dynamics: str = "double_integrator", filter_o
     rec = hot + a16(8 * 12) + a16(8 * 6 * NL) + a16(4 * (NL * (NL - 1) // 2))
     state_r = rec + N * 4
     state_w = hot
-    outputs = N * OBS * 4 + N * E * F * 4 + N * E * E * 4 + N * 4 + N + 1 + N * 16 * 8 + 4 * N * 8
+    outputs = N * OBS * 4 + N * E * F * 4 + N * E * E * 4 + N * 4 + N + 1 + N * 18 * 8 + 4 * N * 8
     hbm = state_r + state_w + outputs
     corners = 16 if di else 32
     gw = 16 if di else 32

@@ -44,6 +44,38 @@ class EnvInfos(list):
     """Per-env info list built lazily from the device info tensor (host copy)."""
 
 
+def infos_from_arrays(info, reset, ep_info, auto_reset=True):
+    """The reference's per-env info lists from the device arrays: per agent the
+    ``info_callback`` dict (navigation_graph_safe.py:386-450) plus the keys
+    ``MultiAgentGraphEnv.step`` adds (environment.py:1025-1029), then the episode summary as
+    the (N+1)-th entry when the worker auto-reset (env_wrappers.py:866-871).
+
+    info [n][N][LSM_INFO_FIELDS] float64 (capi.INFO_FIELDS), reset [n], ep_info [n][8] or None.
+    """
+    fields = capi.INFO_FIELDS
+    n, N = info.shape[0], info.shape[1]
+    out = []
+    for e in range(n):
+        lst = EnvInfos()
+        for i in range(N):
+            d = {k: float(info[e, i, j]) for j, k in enumerate(fields) if not k.startswith("position_")}
+            d["Safety filtered"] = bool(d["Safety filtered"])
+            d["Safety violated"] = bool(d["Safety violated"])
+            d["id"] = i
+            d["position"] = np.array([info[e, i, fields.index("position_x")],
+                                      info[e, i, fields.index("position_y")]], dtype=np.float64)
+            d["Num_obst_collisions"] = 0.0
+            d["Mean_by_variance"] = d["Distance_mean"] / (d["Distance_variance"] + 0.0001)
+            d["Time_taken"] = d["Time_req_to_goal"]
+            d["Time_mean_by_stddev"] = d["Time_mean"] / (d["Time_stddev"] + 0.0001)
+            d["Departed"] = True
+            lst.append(d)
+        if auto_reset and reset[e]:
+            lst.append({k: float(ep_info[e, j]) for j, k in enumerate(EPKEYS)})
+        out.append(lst)
+    return tuple(out)
+
+
 class GpuGraphVecEnv:
     def __init__(self, all_args, num_envs: Optional[int] = None, device=None,
                  value_table: Optional[HjTable] = None, ttr_table: Optional[HjTable] = None,
@@ -230,25 +262,9 @@ class GpuGraphVecEnv:
         return self.step_wait()
 
     def _infos(self):
-        info = self.t_info.cpu().numpy()
         reset = self.t_reset.cpu().numpy()
-        ep = self.t_epinfo.cpu().numpy() if reset.any() else None
-        fields = capi.INFO_FIELDS
-        out = []
-        for e in range(self.num_envs):
-            lst = EnvInfos()
-            for i in range(self.N):
-                d = {k: float(info[e, i, j]) for j, k in enumerate(fields)}
-                d["Safety filtered"] = bool(d["Safety filtered"])
-                d["Safety violated"] = bool(d["Safety violated"])
-                d["id"] = i
-                d["Departed"] = True
-                d["Num_obst_collisions"] = 0.0
-                lst.append(d)
-            if self.auto_reset and reset[e]:
-                lst.append({k: float(ep[e, j]) for j, k in enumerate(EPKEYS)})
-            out.append(lst)
-        return tuple(out)
+        return infos_from_arrays(self.t_info.cpu().numpy(), reset,
+                                 self.t_epinfo.cpu().numpy() if reset.any() else None, self.auto_reset)
 
     def set_agent_state(self, env_index: int, agent_state, reached=None):
         """Overwrite one env's agent states ([N][4]) and optionally reached_goal ([N])."""

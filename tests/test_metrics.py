@@ -1,0 +1,91 @@
+"""Runner metrics from the info tensor (lsm/metrics.py) vs the reference's per-dict path:
+``GpuGraphVecEnv`` info dicts (lsm.vec_env.infos_from_arrays) fed through a restatement of
+``BaseRunner.process_infos`` (onpolicy/runner/shared/base_runner.py:222-301) and ``log_env``'s
+np.mean (:317-331). CPU only (the arrays stand in for the device tensor)."""
+import os
+import sys
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(os.path.dirname(HERE), "layered-safe-marl_amd"))
+
+from lsm import capi, metrics  # noqa: E402
+from lsm.vec_env import infos_from_arrays, EPKEYS  # noqa: E402
+
+
+def _reference_process_infos(infos, num_agents, episode_length, dt):
+    """base_runner.py:222-301, key for key (dt passed in: the runner never sets self.dt)."""
+    src = [("individual_reward", "individual_rewards"), ("Dist_to_goal", "dist_to_goal"),
+           ("Num_agent_collisions", "num_agent_collisions"), ("Num_obst_collisions", "num_obstacle_collisions"),
+           ("Min_time_to_goal", "min_time_to_goal"), ("Distance_mean", "distance_mean"),
+           ("Distance_variance", "distance_variance"), ("Mean_by_variance", "mean_variance"),
+           ("Dists_traveled", "dists_traveled"), ("Time_taken", "time_taken"),
+           ("Formation_dist", "formation_dist"), ("Time_mean", "time_mean"), ("Time_stddev", "time_variance"),
+           ("Time_mean_by_stddev", "time_mn_by_stddev")]
+    out = {}
+    for a in range(num_agents):
+        lists = {dst: [] for _, dst in src}
+        lists["time_to_goal"] = []
+        for info in infos:
+            d = info[a]
+            for k, dst in src:
+                if k in d:
+                    lists[dst].append(d[k])
+            if "Time_req_to_goal" in d:
+                t = d["Time_req_to_goal"]
+                lists["time_to_goal"].append(episode_length * dt if t == -1 else t)
+        for k, v in lists.items():
+            out["agent%d/%s" % (a, k)] = v
+    return out
+
+
+def _arrays(n=6, N=3, seed=0):
+    rng = np.random.default_rng(seed)
+    info = rng.uniform(0, 5, (n, N, len(capi.INFO_FIELDS)))
+    tr = capi.INFO_FIELDS.index("Time_req_to_goal")
+    info[::2, :, tr] = -1.0
+    info[:, :, capi.INFO_FIELDS.index("Distance_variance")] = 0.0   # the +0.0001 guard matters
+    reset = np.zeros(n, dtype=bool)
+    reset[1] = True
+    ep = rng.uniform(0, 1, (n, 8))
+    return info, reset, ep
+
+
+def test_info_dicts_carry_every_reference_key():
+    info, reset, ep = _arrays()
+    infos = infos_from_arrays(info, reset, ep)
+    need = {"id", "position", "min_relative_distance", "Dist_to_goal", "Time_req_to_goal", "Num_agent_collisions",
+            "Num_obst_collisions", "Distance_mean", "Distance_variance", "Mean_by_variance", "Dists_traveled",
+            "Time_taken", "Time_mean", "Time_stddev", "Time_mean_by_stddev", "Min_time_to_goal", "Departed",
+            "Safety filtered", "Safety violated", "individual_reward"}
+    for lst in infos:
+        for d in lst[:3]:
+            assert need <= set(d), need - set(d)
+    assert len(infos[1]) == 4 and set(infos[1][3]) == set(EPKEYS)
+    assert len(infos[0]) == 3
+    px = capi.INFO_FIELDS.index("position_x")
+    np.testing.assert_array_equal(infos[2][1]["position"], info[2, 1, px:px + 2])
+
+
+def test_process_infos_equals_reference_restatement():
+    info, reset, ep = _arrays()
+    N, L, dt = 3, 250, 0.1
+    ref = _reference_process_infos(infos_from_arrays(info, reset, ep), N, L, dt)
+    got = metrics.process_infos(info, N, L, dt)
+    assert set(got) == set(ref)
+    for k in ref:
+        assert got[k] == ref[k], k
+
+
+def test_log_means_on_device_tensor():
+    info, reset, ep = _arrays(n=9, N=4, seed=3)
+    N, L, dt = 4, 350, 1.0
+    ref = _reference_process_infos(infos_from_arrays(info, reset, ep), N, L, dt)
+    got = metrics.log_means(torch.tensor(info), N, L, dt)
+    for k, v in ref.items():
+        if not v:
+            assert k not in got
+            continue
+        np.testing.assert_allclose(got[k], np.mean(v), rtol=1e-12, atol=1e-12, err_msg=k)
