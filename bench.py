@@ -9,7 +9,7 @@ layout (per-ego node_obs / adjacency). Multi-GPU: one process per GPU (torchrun)
 envs sharded by global index (weak scaling), RCCL all_reduce of the episode
 summary at each episode boundary, max-over-ranks timing.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4|5]
 """
 from __future__ import annotations
 
@@ -38,6 +38,10 @@ CONFIGS = {
     4: dict(workload="16-agent airtaxi (Dubins), 8192 envs per GPU, HJ safety filter on",
             dynamics_type="airtaxi", num_agents=16, envs=8192, use_safety_filter=True,
             world_size=6, episode_length=350),
+    5: dict(workload="64-agent double-integrator, 8192 envs per GPU (65536 over 8 GPUs), HJ safety filter "
+                     "on, compact adjacency", dynamics_type="double_integrator", num_agents=64, envs=8192,
+            use_safety_filter=True, world_size=4, episode_length=250, adj_layout="compact",
+            cpu_sample=(1, 30)),   # the oracle takes ~0.5 s per 64-agent env-step: 1 env x 30 steps per core
 }
 
 
@@ -128,7 +132,8 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         cores = a.cpu_cores or min(16, len(os.sched_getaffinity(0)))
-        cpu = cpu_baseline(args, table_dict(vt), table_dict(tt), ep, cores)
+        epw, csteps = c.get("cpu_sample", (4, 500))
+        cpu = cpu_baseline(args, table_dict(vt), table_dict(tt), ep, cores, envs_per_worker=epw, steps=csteps)
 
     import torch
     import torch.distributed as dist
@@ -138,8 +143,9 @@ def main():
     dev = torch.device("cuda:%d" % local_rank)
     torch.cuda.set_device(dev)
     from lsm.vec_env import GpuGraphVecEnv
+    layout = c.get("adj_layout", "reference")
     env = GpuGraphVecEnv(args, num_envs=n_envs, device=dev, value_table=vt, ttr_table=tt,
-                         env_offset=rank * n_envs, return_numpy=False, build_infos=False)
+                         env_offset=rank * n_envs, return_numpy=False, build_infos=False, adj_layout=layout)
     N = c["num_agents"]
     gen = torch.Generator(device=dev).manual_seed(1234 + rank)
     # Synthetic policy: every step's discrete actions drawn up front, resident in HBM before the
@@ -183,7 +189,7 @@ def main():
     total_agent_steps = world * n_envs * N * a.steps
     value = total_agent_steps / elapsed
     from lsm.perf_model import step_bytes
-    sb = step_bytes(N, 2, c["dynamics_type"], c["use_safety_filter"])
+    sb = step_bytes(N, 2, c["dynamics_type"], c["use_safety_filter"], layout)
     bytes_launch = sb["hbm_bytes"] * n_envs
     achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
     traffic = load_traffic(a.config, n_envs)
@@ -195,12 +201,15 @@ def main():
             "config": {"workload": c["workload"], "num_agents": N, "envs_per_gpu": n_envs,
                        "total_envs": world * n_envs, "dynamics": c["dynamics_type"],
                        "safety_filter": c["use_safety_filter"], "episode_length": epl,
-                       "output_layout": "reference (per-ego node_obs/adj, fp32)",
+                       "output_layout": ("reference (per-ego node_obs/adj, fp32)" if layout == "reference" else
+                                         "per-ego node_obs fp32; compact adjacency (E x E fp32 + per-ego "
+                                         "u64 disconnect masks, lossless)"),
                        "hj_table": "synthetic %s" % (str(vt.shape) if vt is not None else "none"),
                        "parallelism": "env-sharded dp%d" % world},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
                          "frac": achieved / PEAK_HBM_GBPS, "traffic": traffic, "traffic_unit": "HBM bytes/launch (rocprofv3 PMC)",
-                         "kernel": "rollout_kernel<%d>" % (0 if c["dynamics_type"] == "double_integrator" else 1),
+                         "kernel": "%s<%d>" % ("rollout_block_kernel" if sb["block"] else "rollout_kernel",
+                                               0 if c["dynamics_type"] == "double_integrator" else 1),
                          "kernel_ms": kern_ms, "algorithmic_bytes_per_launch": bytes_launch,
                          "gather_bytes_per_launch": sb["gather_bytes"] * n_envs},
             "cpu_baseline": cpu,

@@ -21,6 +21,9 @@
  *                        worker's auto-reset on np.all(done) (env_wrappers.py:866-871)
  *   lsm_last_error       exception text (Python wrapper raises RuntimeError)
  *
+ * Kernels: N <= 32 and N * (1 + L) <= 64 run one 64-lane wavefront per env; larger envs
+ * (up to N = 64, E = 256: BASELINE config 5) one 256-thread workgroup per env.
+ *
  * All pointers passed to lsm_step / lsm_bind_output are DEVICE pointers.
  * Calls are stream-ordered and asynchronous; a handle is not thread-safe.
  * Return value: 0 on success, nonzero error code (see lsm_last_error).
@@ -44,7 +47,7 @@ enum { LSM_ACTIONS_INDEX_I32 = 0, LSM_ACTIONS_ONEHOT_F32 = 1, LSM_ACTIONS_ONEHOT
 enum {
   LSM_OUT_OBS = 0,        /* float32 [n][N][OBS]   OBS = 7 (DI) / 6 (airtaxi)       */
   LSM_OUT_NODE_OBS = 1,   /* float32 [n][N][E][F]  F = 10 (DI) / 11 (airtaxi)       */
-  LSM_OUT_ADJ = 2,        /* float32 [n][N][E][E]                                   */
+  LSM_OUT_ADJ = 2,        /* float32 [n][N][E][E] (adj_layout 0) or [n][E][E] (1)    */
   LSM_OUT_REWARD = 3,     /* float32 [n][N]                                         */
   LSM_OUT_DONE = 4,       /* uint8   [n][N]                                         */
   LSM_OUT_RESET_FLAG = 5, /* uint8   [n]      env auto-reset during the last step   */
@@ -53,8 +56,18 @@ enum {
   LSM_OUT_EDGES = 8,      /* uint8   [n][E][E] update_graph() connectivity (optional)*/
   LSM_OUT_STATE = 9,      /* float64 [n][N][4] agent state after the last call      */
   LSM_OUT_DEBUG_STAMPS = 10, /* uint64 [n][16] per-phase clock stamps (diagnostic build only) */
-  LSM_NUM_OUT = 11
+  LSM_OUT_ADJ_MASK = 11,  /* uint64  [n][N][W] per-ego disconnect bits, W = ceil(E/64)
+                             (adj_layout 1 only): bit r of ego e = entity r masked      */
+  LSM_NUM_OUT = 12
 };
+
+/* Adjacency output layouts (lsm_config.adj_layout).
+ *  0  reference: adj[e][r][c] per ego, what graph_observation returns
+ *     (navigation_graph_safe.py:932-994) and the runner's buffer stores (graph_buffer.py:95-104).
+ *  1  compact: the unmasked thresholded distance table A[r][c] (d if 0 < d < range, else 0)
+ *     once per env plus per-ego disconnect masks M[e]; the reference array is
+ *     adj[e][r][c] = (M[e] bit r | M[e] bit c) ? 0 : A[r][c]  (lossless; N x fewer bytes). */
+enum { LSM_ADJ_REFERENCE = 0, LSM_ADJ_COMPACT = 1 };
 
 /* Per-agent info fields (navigation_graph_safe.py:386-450 + environment.py:1025). */
 enum {
@@ -77,7 +90,7 @@ typedef struct lsm_config {
   int32_t use_masking;       /* args.use_masking                                       */
   int32_t auto_reset;        /* 1: GraphSubprocVecEnv worker semantics, 0: Dummy       */
   int32_t emit_edges;        /* 1: fill LSM_OUT_EDGES at the start of each step        */
-  int32_t reserved0;
+  int32_t adj_layout;        /* LSM_ADJ_REFERENCE / LSM_ADJ_COMPACT                    */
   double world_size;         /* args.world_size                                        */
   int64_t seed;              /* env k (global index env_offset + k) seeded seed+1000*k */
   int64_t env_offset;

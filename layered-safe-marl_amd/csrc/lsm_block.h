@@ -1,0 +1,401 @@
+// lsm_block.h -- the workgroup-per-env rollout kernel (included by lsm_rollout.hip inside
+// namespace lsm, after the one-wave kernel whose per-agent functions it reuses).
+//
+// The one-wave kernel keeps an env's E x E distance table, its N x N pair tables and one
+// 64-bit disconnect mask per ego in one wave's LDS, so it stops at N <= 32, E <= 64.
+// BASELINE config 5 (64 double-integrator agents, E = 192, 8192 envs per GPU) needs more;
+// here one 256-thread workgroup (4 waves, one per SIMD) runs one env:
+//   * pair work (the filter's HJ value lookups, the distance reductions of
+//     update_agent_min_relative_distance / is_collision / the episode statistics) runs T =
+//     256 / N threads per ego (a power of two <= 64, so an ego's threads sit in one wave):
+//     each takes every T-th other agent and the partial argmin / min / counts are combined by
+//     a butterfly over the T lanes -- no N x N table in LDS. Ties go to the lower agent
+//     index, i.e. np.argmin's first occurrence (safety_filter.py:395-405);
+//   * no E x E table: the adjacency is computed from an entity-position table in LDS as it
+//     is stored (reference layout: masked for every ego; compact layout: once, plus the
+//     per-ego disconnect masks);
+//   * disconnect masks are ceil(E / 64) words per ego, built from two ballots (entity
+//     flags before / after the reward update) and the snapshot-rule selector.
+// Per-agent phases (integration, obs / reward, info) are the one-wave kernel's functions
+// run by threads 0..N-1; the reset is the same reset_core.
+
+// threads per ego in the pair passes: the largest power of two T <= 64 with T * N <= BT
+__host__ __device__ constexpr int block_tpe(int N) {
+  return (64 * N <= BT) ? 64 : (32 * N <= BT) ? 32 : (16 * N <= BT) ? 16 : (8 * N <= BT) ? 8 : (4 * N <= BT) ? 4 : (2 * N <= BT) ? 2 : 1;
+}
+
+__device__ __forceinline__ bool mbit(const uint64_t* m, int k) { return (m[k >> 6] >> (k & 63)) & 1ull; }
+
+// entity k disconnected (navigation_graph_safe.py:976-989): a done agent, or landmark
+// l = o * N + j already reached by its agent j (reached_goal[j] > o)
+template <bool POST>
+__device__ __forceinline__ bool entity_disc(const Lds& S, int N, int E, int k) {
+  if (k >= E) return false;
+  if (k < N) return (POST ? S.dpost[k] : S.dpre[k]) != 0;
+  const int l = k - N, o = l / N, j = l - o * N;
+  return (POST ? S.rpost[j] : S.rpre[j]) > o;
+}
+
+// S.mpre / S.mpost: entity k = thread k, word w = wave w (E <= BT). All threads call.
+__device__ __forceinline__ void mask_words(const Lds& S, int N, int E) {
+  const int tid = threadIdx.x;
+  const uint64_t bpre = __ballot(entity_disc<false>(S, N, E, tid));
+  const uint64_t bpost = __ballot(entity_disc<true>(S, N, E, tid));
+  if ((tid & 63) == 0) {
+    S.mpre[tid >> 6] = bpre;
+    S.mpost[tid >> 6] = bpost;
+  }
+}
+
+// bits [lo, hi) that fall in word w
+__device__ __forceinline__ uint64_t range_bits(int lo, int hi, int w) {
+  const int a = lo > 64 * w ? lo : 64 * w;
+  const int b = hi < 64 * w + 64 ? hi : 64 * w + 64;
+  if (a >= b) return 0ull;
+  const int n = b - a;
+  return (n == 64 ? ~0ull : ((1ull << n) - 1ull)) << (a - 64 * w);
+}
+
+// entities whose agent j <= e (agents, then landmark orders: N + o N + j): the ones ego e
+// sees after their reward update (sequential snapshot rule)
+__device__ __forceinline__ uint64_t post_sel(int N, int L, int e, int w) {
+  uint64_t m = 0ull;
+  for (int s = 0; s <= L; ++s) m |= range_bits(s * N, s * N + e + 1, w);
+  return m;
+}
+
+// Discrete(25) action of agent `lane` (environment.py:386-410): argmax of a one-hot row or
+// an index
+__device__ __forceinline__ int load_action(const KStep& K, int env, int N, int lane) {
+  int ai = 0;
+  const size_t base = (size_t)env * N + lane;
+  if (K.action_kind == LSM_ACTIONS_INDEX_I32) {
+    ai = ((const GAS int32_t*)gptr(K.actions))[base];
+  } else if (K.action_kind == LSM_ACTIONS_ONEHOT_F32) {
+    const GAS float* a = (const GAS float*)gptr(K.actions) + base * 25;
+    float best = a[0];
+    for (int q = 1; q < 25; ++q) if (a[q] > best) { best = a[q]; ai = q; }
+  } else {
+    const GAS double* a = (const GAS double*)gptr(K.actions) + base * 25;
+    double best = a[0];
+    for (int q = 1; q < 25; ++q) if (a[q] > best) { best = a[q]; ai = q; }
+  }
+  return ai;
+}
+
+// entity positions (agents at their current state, then landmarks)
+template <int NT>
+__device__ __forceinline__ void entity_table(const KParams& P, Lds& S) {
+  constexpr int DYN = 0;
+  LSM_DIMS;
+  for (int k = threadIdx.x; k < E; k += BT) {
+    S.ex[k] = k < N ? S.ps[k] : S.lm[k - N];
+    S.ey[k] = k < N ? S.ps[N + k] : S.lm[NL + k - N];
+  }
+}
+
+// thresholded distance of entities r, c (adj = d * (d < range) * (d > 0),
+// navigation_graph_safe.py:991-992; |p_r - p_c| == |p_c - p_r| bit for bit)
+__device__ __forceinline__ float adj_value(const KParams& P, const Lds& S, int r, int c) {
+  const double dx = S.ex[r] - S.ex[c], dy = S.ey[r] - S.ey[c];
+  const double d = sqrt(dx * dx + dy * dy);
+  return (d < P.coord_range && d > 0) ? (float)d : 0.0f;
+}
+
+// node_obs + adjacency of one env (emission at a step end or after a reset). Expects the
+// entity table, S.emask (per ego) and the pre / post flags.
+template <int DYN, int NT>
+__device__ __forceinline__ void emit_graph_block(const KParams& P, Lds& S, int env) {
+  const int tid = threadIdx.x;
+  LSM_DIMS;
+  const int MW = (E + 63) >> 6;
+  if (DYN == 0) build_rows_di<BT, NT>(P, S); else trig_table_at<BT, NT>(P, S);
+  const bool uni = __syncthreads_and(tid >= N || (S.dpre[tid] == S.dpost[tid] && S.rpre[tid] == S.rpost[tid]));
+  const int EE = E * E;
+  if (P.adj_compact) {
+    GAS float* a = gptr(P.o.adj) + (size_t)env * EE;
+    if ((E & 3) == 0) {
+      for (int t = tid; t < EE / 4; t += BT) {
+        const int u = 4 * t;
+        const int r = qdiv<NT>(u, E, P.m_E), c = u - r * E;
+        st_stream(a + u, make_float4(adj_value(P, S, r, c), adj_value(P, S, r, c + 1), adj_value(P, S, r, c + 2),
+                                     adj_value(P, S, r, c + 3)));
+      }
+    } else {
+      for (int u = tid; u < EE; u += BT) {
+        const int r = qdiv<NT>(u, E, P.m_E), c = u - r * E;
+        a[u] = adj_value(P, S, r, c);
+      }
+    }
+    GAS uint64_t* mo = gptr(P.o.adjmask) + (size_t)env * N * MW;
+    for (int k = tid; k < N * MW; k += BT) mo[k] = S.emask[k];
+  } else {
+    GAS float* adj_out = gptr(P.o.adj) + (size_t)env * N * EE;
+    if ((E & 3) == 0) {
+      // each thread owns float4 column groups of the E x E table: values computed once,
+      // masked per ego (once when every ego shares the mask) and stored for every ego
+      for (int t = tid; t < EE / 4; t += BT) {
+        const int u = 4 * t;
+        const int r = qdiv<NT>(u, E, P.m_E), c = u - r * E;
+        const float4 v = make_float4(adj_value(P, S, r, c), adj_value(P, S, r, c + 1), adj_value(P, S, r, c + 2),
+                                     adj_value(P, S, r, c + 3));
+#pragma unroll 1
+        for (int e = 0; e < N; ++e) {
+          const uint64_t* m = S.emask + (uni ? 0 : e * MW);
+          const uint32_t bits = mbit(m, r) ? 0xfu : (uint32_t)((m[c >> 6] >> (c & 63)) & 0xfull);
+          float4 w = v;
+          if (bits & 1u) w.x = 0.f;
+          if (bits & 2u) w.y = 0.f;
+          if (bits & 4u) w.z = 0.f;
+          if (bits & 8u) w.w = 0.f;
+          st_stream(adj_out + (size_t)e * EE + u, w);
+        }
+      }
+    } else {
+      for (int q = tid; q < N * EE; q += BT) {
+        const int e = qdiv<NT>(q, EE, P.m_EE);
+        const int u = q - e * EE;
+        const int r = qdiv<NT>(u, E, P.m_E), c = u - r * E;
+        const uint64_t* m = S.emask + e * MW;
+        adj_out[q] = (mbit(m, r) || mbit(m, c)) ? 0.0f : adj_value(P, S, r, c);
+      }
+    }
+  }
+  emit_nodes<DYN, BT, NT>(P, S, env, uni);
+}
+
+template <int DYN, int NT>
+__device__ __forceinline__ void reset_block(const KParams& P, Lds& S, int env, const double* cur_new) {
+  const int tid = threadIdx.x;
+  LSM_DIMS;
+  reset_core<DYN, BT, NT>(P, S, env, cur_new);   // ends with a barrier
+  const int MW = (E + 63) >> 6;
+  for (int k = tid; k < N * MW; k += BT) S.emask[k] = 0ull;
+  entity_table<NT>(P, S);
+  if (tid < N) write_obs<DYN, NT>(P, S, env, tid);
+  __syncthreads();
+  emit_graph_block<DYN, NT>(P, S, env);
+}
+
+template <int DYN, int NT>
+__global__ __launch_bounds__(BT) void rollout_block_kernel(const KParams* __restrict__ Pp, const KStep K) {
+  const KParams& P = *Pp;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int env = blockIdx.x;
+  const int tid = threadIdx.x;
+  if (env >= P.n_envs) return;   // uniform over the workgroup
+  LSM_DIMS;
+  const int MW = (E + 63) >> 6;
+  constexpr int T = NT ? block_tpe(NT) : 64;      // butterfly bound (generic: up to 64 lanes)
+  const int TE = NT ? T : block_tpe(N);           // threads per ego actually used
+  Lds S = carve_block(smem, N, NL, E, F);
+
+  // ---- 0. the env's record HBM -> LDS + this step's actions ------------------------------
+  const int ai = (K.mode == 0 && tid < N) ? load_action(K, env, N, tid) : 0;
+  rec_copy<BT>((const GAS f32x4*)gptr(P.s.rec) + (size_t)env * P.s.rec_stride16, (f32x4*)smem, P.s.rec16);
+  __syncthreads();
+  if (tid < N) {
+    S.dpre[tid] = S.dpost[tid];
+    S.rpre[tid] = S.rpost[tid];
+    if (DYN == 1) {
+      S.ecs[tid] = cos(S.ps[2 * N + tid]);
+      S.ecs[N + tid] = sin(S.ps[2 * N + tid]);
+    }
+  }
+  const int cstep = S.step[0] + 1;
+  __syncthreads();
+
+  if (K.mode == 1) {
+    reset_block<DYN, NT>(P, S, env, K.cur_new);
+    __syncthreads();
+    store_state<DYN, BT, NT>(P, S, smem, env, true);
+    return;
+  }
+
+  // ---- 1. update_graph() at step start (previous state, final masks) ----------------------
+  if (K.emit_edges) {
+    entity_table<NT>(P, S);
+    mask_words(S, N, E);
+    __syncthreads();
+    GAS uint8_t* eo = gptr(P.o.edges) + (size_t)env * E * E;
+    const bool fresh = S.step[1] != 0;   // lsm_set_agent_state: calculate_distances() unmasked
+    for (int u = tid; u < E * E; u += BT) {
+      const int a = qdiv<NT>(u, E, P.m_E), b = u - a * E;
+      const double dx = S.ex[a] - S.ex[b], dy = S.ey[a] - S.ey[b];
+      double d = sqrt(dx * dx + dy * dy);
+      if (!fresh && (mbit(S.mpost, a) || mbit(S.mpost, b))) d = 0.0;
+      eo[u] = (d <= P.coord_range && d > 0) ? 1 : 0;
+    }
+  }
+
+  // ---- 2. decode actions ----------------------------------------------------------------
+  if (tid < N) {
+    const int a = ai < 0 ? 0 : (ai > 24 ? 24 : ai);
+    const int xi = a / 5, yi = a - xi * 5;
+    S.raw[tid] = P.act0[xi];
+    S.raw[N + tid] = P.act1[yi];
+  }
+  __syncthreads();
+
+  // ---- 3. safety filter: T threads per ego, butterfly argmins --------------------------------
+  const bool filter_on = S.cur[C_FILT] != 0.0;
+  if (filter_on) {
+    const int i = tid / TE, q = tid - (tid / TE) * TE;
+    int jd = -1, jv = -1, okv = 0;
+    double dmin = 0.0;
+    float vmin = 0.0f;
+    const bool ego = i < N && !S.dpre[i];
+    if (ego) {
+#pragma unroll 1
+      for (int j = q; j < N; j += TE) {
+        if (j == i || S.dpre[j]) continue;
+        const double ex = S.ps[i], ey = S.ps[N + i], ox = S.ps[j], oy = S.ps[N + j];
+        const double d = sqrt((ox - ex) * (ox - ex) + (oy - ey) * (oy - ey));
+        double rel[5];
+        rel_state<DYN>(S, N, i, j, rel);
+        float v = 0.0f;
+        bool ok;
+        if (DYN == 0) ok = interp_value<4>(P.val, rel, v); else ok = interp_value<5>(P.val, rel, v);
+        if (!ok) v = INFINITY;
+        if (jd < 0 || d < dmin) { jd = j; dmin = d; }
+        if (jv < 0 || v < vmin) { jv = j; vmin = v; okv = ok ? 1 : 0; }
+      }
+    }
+#pragma unroll
+    for (int off = 1; off < T; off <<= 1) {
+      if (off >= TE) break;
+      const int jd2 = __shfl_xor(jd, off), jv2 = __shfl_xor(jv, off), ok2 = __shfl_xor(okv, off);
+      const double d2 = __shfl_xor(dmin, off);
+      const float v2 = __shfl_xor(vmin, off);
+      if (jd2 >= 0 && (jd < 0 || d2 < dmin || (d2 == dmin && jd2 < jd))) { jd = jd2; dmin = d2; }
+      if (jv2 >= 0 && (jv < 0 || v2 < vmin || (v2 == vmin && jv2 < jv))) { jv = jv2; vmin = v2; okv = ok2; }
+    }
+    if (q == 0 && i < N) {
+      double u0 = S.raw[i], u1 = S.raw[N + i];
+      uint8_t fl = 0;
+      int dec = -1;
+      if (ego && jd >= 0) {   // else: no other active agent
+        dec = jv;
+        if (!(dmin > P.coord_range) && okv) filter_apply<DYN, NT>(P, S, i, jv, vmin, fl, u0, u1);
+      }
+      S.sfilt[i] = fl;
+      S.decon[i] = dec;
+      S.safe[i] = u0;
+      S.safe[N + i] = u1;
+      S.adiff[i] = blas_norm2(S.raw[i] - u0, S.raw[N + i] - u1);
+    }
+  } else if (tid < N) {
+    const double u0 = S.raw[tid], u1 = S.raw[N + tid];
+    S.safe[tid] = u0;
+    S.safe[N + tid] = u1;
+    S.adiff[tid] = blas_norm2(S.raw[tid] - u0, S.raw[N + tid] - u1);
+  }
+  __syncthreads();
+
+  // ---- 4. integrate ------------------------------------------------------------------------
+  if (tid < N && !S.dpre[tid]) integrate_agent<DYN>(P, S, N, tid);
+  __syncthreads();
+  entity_table<NT>(P, S);
+
+  // ---- 5. min relative distance (active agents) and is_collision counts (all agents) ------
+  {
+    const int i = tid / TE, q = tid - (tid / TE) * TE;
+    double m = INFINITY;
+    int cc = 0;
+    if (i < N) {
+      const bool iact = !S.dpre[i];
+#pragma unroll 4
+      for (int j = q; j < N; j += TE) {
+        if (j == i) continue;
+        const double d2 = blas_norm2(S.ps[i] - S.ps[j], S.ps[N + i] - S.ps[N + j]);
+        if (iact && !S.dpre[j]) m = (d2 < m) ? d2 : m;
+        if (d2 < 1.05 * (0.05 + 0.05)) cc++;
+      }
+    }
+#pragma unroll
+    for (int off = 1; off < T; off <<= 1) {
+      if (off >= TE) break;
+      const double o = __shfl_xor(m, off);
+      m = (o < m) ? o : m;
+      cc += __shfl_xor(cc, off);
+    }
+    if (q == 0 && i < N) {
+      S.minrel[i] = m;
+      S.ccnt[i] = cc;
+    }
+  }
+
+  // ---- 6. obs, reward, goal/done update ---------------------------------------------------
+  double mag = 0.0;
+  if (DYN == 0 && !P.use_filter_arg) mag = magnetic_penalty_wave<BT, NT>(P, S, S.dpair);   // has barriers
+  AgentTmp at;
+  if (tid < N) reward_agent<DYN, NT>(P, S, env, tid, mag, at);
+  __syncthreads();
+  mask_words(S, N, E);
+  __syncthreads();
+  for (int k = tid; k < N * MW; k += BT) {
+    const int e = k / MW, w = k - e * MW;
+    const uint64_t sel = post_sel(N, L, e, w);
+    S.emask[k] = (S.mpost[w] & sel) | (S.mpre[w] & ~sel);
+  }
+
+  // ---- 7/8. info_callback numbers -----------------------------------------------------------
+  if (tid < N) info_agent<DYN, NT>(P, S, tid, cstep, at, S.ccnt[tid]);
+  __syncthreads();
+  if (tid < N) info_row<NT>(P, S, tid, at.rew, S.dpair + tid * LSM_INFO_FIELDS);
+  __syncthreads();
+  rec_copy<BT>((const f32x4*)S.dpair, (GAS f32x4*)(gptr(P.o.info) + (size_t)env * N * LSM_INFO_FIELDS),
+               N * LSM_INFO_FIELDS / 2);
+
+  // ---- episode stats (environment.py:1004-1022), dones -------------------------------------
+  {
+    const int i = tid / TE, q = tid - (tid / TE) * TE;
+    int cnt = 0, neng = 0;
+    double mn = INFINITY;
+    const bool act = i < N && !S.dpost[i];   // departed is always True in the training scenario
+    if (act) {
+      const uint64_t* m = S.emask + i * MW;
+      const bool mi = mbit(m, i);
+#pragma unroll 4
+      for (int j = q; j < N; j += TE) {
+        if (mi || mbit(m, j)) continue;
+        const double dx = S.ps[i] - S.ps[j], dy = S.ps[N + i] - S.ps[N + j];
+        const double d = sqrt(dx * dx + dy * dy);
+        if (!(d < P.coord_range && d > 0)) continue;
+        cnt++;
+        if (d < P.world_eng) neng++;
+        mn = (d < mn) ? d : mn;
+      }
+    }
+#pragma unroll
+    for (int off = 1; off < T; off <<= 1) {
+      if (off >= TE) break;
+      const double o = __shfl_xor(mn, off);
+      mn = (o < mn) ? o : mn;
+      cnt += __shfl_xor(cnt, off);
+      neng += __shfl_xor(neng, off);
+    }
+    if (q == 0 && act) stats_agent<DYN>(P, S, N, i, cnt, neng, mn);
+  }
+  bool my_done = true;
+  if (tid < N) {
+    if (S.dpost[tid]) S.stats[2 * N + tid] = 1;
+    my_done = S.dpost[tid] || cstep >= P.episode_length;
+    gptr(P.o.dones)[(size_t)env * N + tid] = my_done ? 1 : 0;
+  }
+  const bool all_done = __syncthreads_and(my_done);
+
+  // ---- 9. graph outputs, or the auto-reset (whose outputs replace them) ---------------------
+  if (tid == 0) { S.step[0] = cstep; S.step[1] = 0; }
+  if (P.auto_reset && all_done) {
+    if (tid == 0) gptr(P.o.reset_flag)[env] = 1;
+    reset_block<DYN, NT>(P, S, env, K.cur_new);
+    __syncthreads();
+    store_state<DYN, BT, NT>(P, S, smem, env, true);
+  } else {
+    if (tid == 0) gptr(P.o.reset_flag)[env] = 0;
+    emit_graph_block<DYN, NT>(P, S, env);
+    __syncthreads();
+    store_state<DYN, BT, NT>(P, S, smem, env, false);
+  }
+}

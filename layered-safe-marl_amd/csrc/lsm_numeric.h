@@ -62,6 +62,26 @@ LSM_HD double np_sum_acc(const A& a, int n) {
   for (; i < n; ++i) res += a(i);
   return res;
 }
+// np_sum_acc over a plain array with the 8-way loop kept rolled (large n, rare path)
+LSM_HD double np_sum_rolled(const double* a, int n) {
+  if (n < 8) {
+    double res = 0.0;
+    for (int i = 0; i < n; ++i) res += a[i];
+    return res;
+  }
+  double r0 = a[0], r1 = a[1], r2 = a[2], r3 = a[3], r4 = a[4], r5 = a[5], r6 = a[6], r7 = a[7];
+  int i = 8;
+#pragma unroll 1
+  for (; i < n - (n % 8); i += 8) {
+    r0 += a[i]; r1 += a[i + 1]; r2 += a[i + 2]; r3 += a[i + 3];
+    r4 += a[i + 4]; r5 += a[i + 5]; r6 += a[i + 6]; r7 += a[i + 7];
+  }
+  double res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
+#pragma unroll 1
+  for (; i < n; ++i) res += a[i];
+  return res;
+}
+LSM_HD double np_mean_rolled(const double* a, int n) { return np_sum_rolled(a, n) / (double)n; }
 struct ArrAcc {
   const double* p;
   LSM_HD double operator()(int i) const { return p[i]; }

@@ -113,10 +113,12 @@ struct OutDev {
   double* info;
   uint8_t* edges;
   double* state;
+  uint64_t* adjmask;   // LSM_OUT_ADJ_MASK (compact adjacency layout)
 };
 
 struct KParams {
   int n_envs, N, L, NL, E, F, OBS, dyn, episode_length, use_masking, use_filter_arg, auto_reset;
+  int adj_compact;   // LSM_ADJ_COMPACT: unmasked E x E table once per env + per-ego masks
   double dt, world_size, coord_range, world_eng, sep_target, max_speed, min_speed, gs_min, gs_max;
   double act0[5], act1[5];
   double mag_c[50], mag_s[50];
@@ -189,6 +191,12 @@ struct Lds {
   double* feat;      // [2N + NL][F] DI entity rows: agents pre, agents post, landmarks
   double* egooff;    // [N][F] DI ego offsets
   float* stage;      // [64][F] airtaxi node staging
+  // workgroup-per-env kernel only (lsm_block.h)
+  double* ex;        // [E] entity x (agents after integration, then landmarks)
+  double* ey;        // [E]
+  int32_t* ccnt;     // [N] is_collision counts of this step
+  uint64_t* mpre;    // [4] disconnect bits before the reward update (entity r = bit r)
+  uint64_t* mpost;   // [4] after
 };
 
 struct LdsPlan {
@@ -198,8 +206,15 @@ struct LdsPlan {
   size_t off[40];
 };
 
+// Workgroup-per-env kernel (lsm_block.h): threads per env and its limits.
+constexpr int BT = 256;
+constexpr int BMAXN = 64;
+constexpr int BMAXE = 256;   // masks: E <= BT so one ballot per wave gives a mask word
+
 // q / d for q * d < 2^32 (all index math here): __umulhi(q, ceil(2^32 / d))
 __device__ __forceinline__ int fdiv(int q, uint32_t m) { return (int)__umulhi((uint32_t)q, m); }
+
+__host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
 
 // Kernels are specialised on the agent count NT (L = 2, the training setting) so every
 // dimension, LDS offset and index division below folds to a constant; NT = 0 is the
@@ -245,10 +260,11 @@ __device__ __forceinline__ bool group_all(bool v) {
   return (b & gm) == gm;
 }
 
-__host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
-
 // Offsets of every LDS array (shared by the host launch/record init and the device carve).
-__host__ __device__ inline LdsPlan lds_plan(int N, int NL, int E, int F) {
+// The record prefix (fields 0..14) is common to both kernels; the workgroup kernel keeps no
+// landmark-distance cache (lmd, 0 bytes), no E x E / N x N tables, and adds the entity
+// position table, per-ego multi-word masks and a node staging area.
+__host__ __device__ inline LdsPlan lds_plan(int N, int NL, int E, int F, bool block = false) {
   LdsPlan p;
   size_t o = 0;
   int k = 0;
@@ -258,11 +274,35 @@ __host__ __device__ inline LdsPlan lds_plan(int N, int NL, int E, int F) {
   put(8 * N); put(8 * N); put(8 * N); put(8 * N);
   put(4 * N); put(4 * N); put(4 * N); put(4 * N); put(8);
   p.hot = o;
-  put(8 * NCUR); put(8 * 6 * NL); put(4 * (NL * (NL - 1) / 2));
+  put(8 * NCUR); put(8 * 6 * NL); put(block ? 0 : 4 * (NL * (NL - 1) / 2));
   p.rec = o;
+  const int MW = (E + 63) / 64;
   // scratch
-  put(4 * N); put(4 * N); put(8 * 2 * N); put(8 * 2 * N); put(8 * 2 * N); put(8 * 2 * N); put(8 * N);
+  put(4 * N); put(4 * N); put(8 * 2 * N); put(8 * 2 * N); put(8 * 2 * N); put(8 * 2 * N);
+  put(block ? 8 * N * MW : 8 * N);
   put(F == 10 ? 0 : 8 * 2 * N);
+  if (block) {
+    // fval aa aa2 -> none; U1 = {mt, scen, scratch} | {feat, egooff} | {pair partials, info rows}
+    put(8 * E); put(8 * E); put(4 * N); put(8 * 8);   // ex, ey, ccnt, mpre[4] + mpost[4]
+    const size_t u1 = o;
+    size_t c = align16(4 * MT_WORDS), d = c + align16(8 * SCEN_WS), e = d + align16(8 * 2 * N);
+    size_t g1 = F == 10 ? align16(8 * (2 * N + NL) * F) : align16(8 * 4 * N);
+    size_t g2 = g1 + (F == 10 ? align16(8 * N * F) : 0);
+    size_t m = 8 * 2 * BT;
+    m = m > (size_t)(8 * LSM_INFO_FIELDS * N) ? m : (size_t)(8 * LSM_INFO_FIELDS * N);
+    size_t u1sz = e > g2 ? e : g2;
+    u1sz = u1sz > align16(m) ? u1sz : align16(m);
+    p.off[k++] = u1; p.off[k++] = u1 + c; p.off[k++] = u1 + d;   // mt, scen, scratch
+    p.off[k++] = u1; p.off[k++] = u1 + g1;                         // feat, egooff
+    p.off[k++] = u1;                                               // dpair: pair partials / info rows
+    o = u1 + u1sz;
+    // node staging (airtaxi, or DI with E * F % 4 != 0): live together with feat
+    const bool stage = F != 10 || ((E * F) & 3) != 0;
+    p.off[k++] = o;
+    o += stage ? align16(4 * BT * F) : 0;
+    p.bytes = o;
+    return p;
+  }
   // U1
   const size_t u1 = o;
   size_t a = align16(4 * E * E), a2 = a + align16(8 * N * N), b = a2 + align16(8 * N * N);
@@ -329,6 +369,54 @@ __device__ __forceinline__ Lds carve(unsigned char* base, int N, int NL, int E, 
   L.feat = (double*)(base + p.off[k++]);
   L.egooff = (double*)(base + p.off[k++]);
   L.stage = (float*)(base + p.off[k++]);
+  L.ex = L.ey = nullptr;
+  L.ccnt = nullptr;
+  L.mpre = L.mpost = nullptr;
+  return L;
+}
+
+// LDS carve of the workgroup-per-env kernel (lds_plan(..., block = true)).
+__device__ __forceinline__ Lds carve_block(unsigned char* base, int N, int NL, int E, int F) {
+  const LdsPlan p = lds_plan(N, NL, E, F, true);
+  Lds L;
+  int k = 0;
+  L.ps = (double*)(base + p.off[k++]);
+  L.stats = (double*)(base + p.off[k++]);
+  L.winfo = (double*)(base + p.off[k++]);
+  L.pdist = (double*)(base + p.off[k++]);
+  L.gmt = (double*)(base + p.off[k++]);
+  L.minrel = (double*)(base + p.off[k++]);
+  L.adiff = (double*)(base + p.off[k++]);
+  L.dpost = (int32_t*)(base + p.off[k++]);
+  L.rpost = (int32_t*)(base + p.off[k++]);
+  L.sfilt = (int32_t*)(base + p.off[k++]);
+  L.decon = (int32_t*)(base + p.off[k++]);
+  L.step = (int32_t*)(base + p.off[k++]);
+  L.cur = (double*)(base + p.off[k++]);
+  L.lm = (double*)(base + p.off[k++]);
+  L.lmsc = L.lm + 4 * NL;
+  L.lmd = nullptr; k++;
+  L.dpre = (int32_t*)(base + p.off[k++]);
+  L.rpre = (int32_t*)(base + p.off[k++]);
+  L.raw = (double*)(base + p.off[k++]);
+  L.safe = (double*)(base + p.off[k++]);
+  L.wold = (double*)(base + p.off[k++]);
+  L.wnew = (double*)(base + p.off[k++]);
+  L.emask = (uint64_t*)(base + p.off[k++]);
+  L.ecs = (double*)(base + p.off[k++]);
+  L.ex = (double*)(base + p.off[k++]);
+  L.ey = (double*)(base + p.off[k++]);
+  L.ccnt = (int32_t*)(base + p.off[k++]);
+  L.mpre = (uint64_t*)(base + p.off[k++]);
+  L.mpost = L.mpre + 4;
+  L.mt = (uint32_t*)(base + p.off[k++]);
+  L.scen = (double*)(base + p.off[k++]);
+  L.scratch = (double*)(base + p.off[k++]);
+  L.feat = (double*)(base + p.off[k++]);
+  L.egooff = (double*)(base + p.off[k++]);
+  L.dpair = (double*)(base + p.off[k++]);
+  L.stage = (float*)(base + p.off[k++]);
+  L.fval = nullptr; L.aa = nullptr; L.aa2 = nullptr; L.vpair = nullptr; L.inr = nullptr;
   return L;
 }
 
@@ -673,6 +761,10 @@ __device__ __forceinline__ void rel_state(const Lds& S, int N, int e, int o, dou
 }
 
 template <int DYN, int NT>
+__device__ __forceinline__ void filter_apply(const KParams& P, const Lds& S, int i, int jv, float vmin,
+                                             uint8_t& filtered, double& u0, double& u1);
+
+template <int DYN, int NT>
 __device__ __forceinline__ void filter_ego(const KParams& P, Lds& S, int i, uint8_t& filtered, int& dec,
                                   double& u0, double& u1) {
   LSM_DIMS;
@@ -694,6 +786,17 @@ __device__ __forceinline__ void filter_ego(const KParams& P, Lds& S, int i, uint
   dec = jv;
   if (dmin > P.coord_range) return;
   if (!S.inr[i * N + jv]) return;
+  filter_apply<DYN, NT>(P, S, i, jv, vmin, filtered, u0, u1);
+}
+
+// The filter for ego i once its deconflicting agent jv (argmin of the HJ value, V = vmin in
+// range) is known and the nearest agent is within the coordination range: gradient lookup,
+// optimal control (V < eps_hj) or the closed-form CBF-QP, clips (safety_filter.py:264-308,
+// 395-433).
+template <int DYN, int NT>
+__device__ __forceinline__ void filter_apply(const KParams& P, const Lds& S, int i, int jv, float vmin,
+                                             uint8_t& filtered, double& u0, double& u1) {
+  LSM_DIMS;
   const int ND = (DYN == 0) ? 4 : 5;
   double rel[5];
   rel_state<DYN>(S, N, i, jv, rel);
@@ -813,7 +916,7 @@ __device__ __forceinline__ void filter_ego(const KParams& P, Lds& S, int i, uint
   }
   u0 = u[0];
   u1 = u[1];
-  (void)ND;
+  (void)ND; (void)E; (void)F;
 }
 
 // ----------------------------------------------------------------------------------
@@ -987,6 +1090,9 @@ __device__ __forceinline__ void emit_adj_uniform(const KParams& P, const Lds& S,
   }
 }
 
+template <int DYN, int LPE, int NT>
+__device__ __forceinline__ void emit_nodes(const KParams& P, Lds& S, int env, bool uni);
+
 // `adj_done`: the uniform adjacency was already stored (speculatively, in chunks during the
 // step); it is rewritten here only if an agent changed status.
 template <int DYN, int LPE, int NT>
@@ -1002,7 +1108,16 @@ __device__ __forceinline__ void emit_graph(const KParams& P, Lds& S, int env, bo
   // ---- adjacency: ego e, row r, col c ------------------------------------------------------
   const int EE = E * E, atot = N * EE;
   GAS float* adj_out = gptr(P.o.adj) + (size_t)env * atot;
-  if ((E & 3) == 0 && uni) {
+  if (P.adj_compact) {
+    // LSM_ADJ_COMPACT: the unmasked table once + the per-ego masks (one word: E <= 64)
+    GAS float* a = gptr(P.o.adj) + (size_t)env * EE;
+    if ((E & 3) == 0) {
+      for (int q = lane; q < EE / 4; q += LPE) st_stream(a + 4 * q, *(const float4*)(S.fval + 4 * q));
+    } else {
+      for (int q = lane; q < EE; q += LPE) a[q] = S.fval[q];
+    }
+    if (lane < N) gptr(P.o.adjmask)[(size_t)env * N + lane] = S.emask[lane];
+  } else if ((E & 3) == 0 && uni) {
     if (!adj_done) emit_adj_uniform<LPE, NT>(P, S, env, S.emask[0], 0, N);
   } else if ((E & 3) == 0) {
     // Each lane owns fixed float4 column groups u of the E x E table (loaded from LDS once)
@@ -1046,7 +1161,15 @@ __device__ __forceinline__ void emit_graph(const KParams& P, Lds& S, int env, bo
       adj_out[q] = (((m >> r) | (m >> c)) & 1ull) ? 0.0f : S.fval[u];
     }
   }
-  // ---- node features --------------------------------------------------------------
+  emit_nodes<DYN, LPE, NT>(P, S, env, uni);
+}
+
+// node_obs [N][E][F] of one env (DI rows / airtaxi trig table already in LDS). `uni`: no
+// agent changed status this step, so every ego sees the post rows.
+template <int DYN, int LPE, int NT>
+__device__ __forceinline__ void emit_nodes(const KParams& P, Lds& S, int env, bool uni) {
+  const int lane = threadIdx.x & (LPE - 1);
+  LSM_DIMS;
   const int npairs = N * E, ntot = npairs * F;
   GAS float* node_out = gptr(P.o.node) + (size_t)env * ntot;
   if (DYN == 0 && ((E * F) & 3) == 0 && uni) {
@@ -1222,8 +1345,8 @@ __device__ __forceinline__ void summary(const KParams& P, const Lds& S, double* 
   const double* cf = S.stats + 3 * N;
   const double* md = S.stats + 4 * N;
   const double* mu = S.stats + 5 * N;
-  double* a = S.scratch;
-  double* b = S.scratch + MAXN;
+  double* a = S.scratch;   // [2][N]
+  double* b = S.scratch + N;
   out[0] = P.dt * np_mean(tl, N);
   out[1] = np_mean(td, N);
   out[2] = np_mean(dn, N);
@@ -1242,16 +1365,55 @@ __device__ __forceinline__ void summary(const KParams& P, const Lds& S, double* 
   if (out[6] == INFINITY) out[6] = P.coord_range;
 }
 
+// summary() with its loops kept rolled (workgroup kernel, N up to 64: unrolled, the scheduler
+// hoists every LDS load of the five pairwise sums and the kernel spills). Same arithmetic.
+template <int NT>
+__device__ __forceinline__ void summary_rolled(const KParams& P, const Lds& S, double* out) {
+  constexpr int DYN = 0;
+  LSM_DIMS;
+  const double* tl = S.stats;
+  const double* td = S.stats + N;
+  const double* dn = S.stats + 2 * N;
+  const double* cf = S.stats + 3 * N;
+  const double* md = S.stats + 4 * N;
+  const double* mu = S.stats + 5 * N;
+  double* a = S.scratch;   // [2][N]
+  double* b = S.scratch + N;
+  out[0] = P.dt * np_mean_rolled(tl, N);
+  out[1] = np_mean_rolled(td, N);
+  out[2] = np_mean_rolled(dn, N);
+#pragma unroll 1
+  for (int i = 0; i < N; ++i) a[i] = (double)S.rpost[i];
+  out[3] = np_mean_rolled(a, N);
+#pragma unroll 1
+  for (int i = 0; i < N; ++i) b[i] = (tl[i] == 0) ? 1.0 : tl[i];
+#pragma unroll 1
+  for (int i = 0; i < N; ++i) a[i] = cf[i] / b[i];
+  out[4] = np_mean_rolled(a, N);
+  out[5] = np_mean_rolled(md, N);
+#pragma unroll 1
+  for (int i = 0; i < N; ++i) a[i] = mu[i] / b[i];
+  out[7] = np_mean_rolled(a, N);
+  if (out[5] == INFINITY) out[5] = P.coord_range;
+  double mn = md[0];
+#pragma unroll 1
+  for (int i = 1; i < N; ++i) mn = (md[i] < mn) ? md[i] : mn;
+  out[6] = mn;
+  if (out[6] == INFINITY) out[6] = P.coord_range;
+}
+
 // Device reset of one env (MultiAgentGraphEnv.reset, environment.py:1046-1074). Expects the
 // env's persistent per-agent arrays in LDS (S.stats, S.rpost = reached_goal before reset).
+// Everything of the reset up to the outputs: summary, curriculum block, scenario draw,
+// per-agent episode arrays.
 template <int DYN, int LPE, int NT>
-__device__ __forceinline__ void reset_env(const KParams& P, Lds& S, int env, const double* cur_new) {
+__device__ __forceinline__ void reset_core(const KParams& P, Lds& S, int env, const double* cur_new) {
   const int lane = threadIdx.x & (LPE - 1);
   LSM_DIMS;
   GAS double* prev = gptr(P.s.prev) + (size_t)env * 8;
   if (lane == 0) {
     double outv[8];
-    summary<NT>(P, S, outv);
+    if (LPE == BT) summary_rolled<NT>(P, S, outv); else summary<NT>(P, S, outv);
     for (int k = 0; k < 8; ++k) {
       prev[k] = outv[k];
       gptr(P.o.ep_info)[(size_t)env * 8 + k] = outv[k];
@@ -1290,6 +1452,13 @@ __device__ __forceinline__ void reset_env(const KParams& P, Lds& S, int env, con
   }
   if (lane == 0) { S.step[0] = 0; S.step[1] = 0; }
   __syncthreads();   // MT words read out of U1 before compute_dist overwrites it
+}
+
+template <int DYN, int LPE, int NT>
+__device__ __forceinline__ void reset_env(const KParams& P, Lds& S, int env, const double* cur_new) {
+  const int lane = threadIdx.x & (LPE - 1);
+  LSM_DIMS;
+  reset_core<DYN, LPE, NT>(P, S, env, cur_new);
   compute_dist<LPE, NT>(P, S, nullptr, true);
   if (lane < N) write_obs<DYN, NT>(P, S, env, lane);
   emit_graph<DYN, LPE, NT>(P, S, env);
@@ -1330,6 +1499,230 @@ __device__ __forceinline__ void store_state(const KParams& P, Lds& S, const unsi
   }
   __syncthreads();
   rec_copy<LPE>((const f32x4*)lbase, (GAS f32x4*)gptr(P.s.rec) + (size_t)env * P.s.rec_stride16, full ? P.s.rec16 : P.s.hot16);
+}
+
+// closed-form integration of agent i, speed clamp, travel distance (core.py:118-131,199-210,680-687)
+template <int DYN>
+__device__ __forceinline__ void integrate_agent(const KParams& P, Lds& S, int N, int i) {
+  const double dt = P.dt;
+  const double a0 = S.safe[i], a1 = S.safe[N + i];
+  double x = S.ps[i], y = S.ps[N + i], s2 = S.ps[2 * N + i], s3 = S.ps[3 * N + i];
+  double spd;
+  if (DYN == 0) {
+    x = x + s2 * dt + 0.5 * a0 * dt * dt;
+    y = y + s3 * dt + 0.5 * a1 * dt * dt;
+    s2 = s2 + a0 * dt;
+    s3 = s3 + a1 * dt;
+    spd = sqrt(s2 * s2 + s3 * s3);
+    if (spd > P.max_speed) {
+      s2 = P.max_speed * s2 / spd;
+      s3 = P.max_speed * s3 / spd;
+    }
+    spd = sqrt(s2 * s2 + s3 * s3);
+  } else {
+    const double th0 = s2, v0 = s3, w = a0, ac = a1;
+    const double th1 = th0 + w * dt;
+    const double v1 = v0 + ac * dt;
+    // stable closed form about the mid-heading (oracle/lsm_oracle.py closed_form_step)
+    const double h = 0.5 * w * dt;
+    const double m = th0 + h;
+    const double cm = cos(m), sm = sin(m);
+    double sc, q;
+    if (fabs(h) < 0.1) {
+      const double h2 = h * h;
+      sc = 1.0 - h2 / 6.0 * (1.0 - h2 / 20.0 * (1.0 - h2 / 42.0 * (1.0 - h2 / 72.0)));
+      q = -h / 3.0 * (1.0 - h2 / 10.0 * (1.0 - h2 / 28.0 * (1.0 - h2 / 54.0)));
+    } else {
+      sc = sin(h) / h;
+      q = (cos(h) - sc) / h;
+    }
+    const double A = v0 * dt + 0.5 * ac * dt * dt;
+    const double B = 0.5 * ac * dt * dt;
+    x = x + (A * cm * sc + B * sm * q);
+    y = y + (A * sm * sc - B * cm * q);
+    s2 = th1;
+    s3 = v1;
+    if (s3 > P.max_speed) s3 = P.max_speed;
+    if (s3 < P.min_speed) s3 = P.min_speed;
+    spd = s3;
+  }
+  S.ps[i] = x; S.ps[N + i] = y; S.ps[2 * N + i] = s2; S.ps[3 * N + i] = s3;
+  S.pdist[i] += spd * dt;
+}
+
+// Per-agent values of the reward phase that the info phase reuses.
+struct AgentTmp {
+  double rew = 0.0, th_pre = 0.0, spd_pre = 0.0, ct_pre = 1.0, st_pre = 0.0;
+  bool reached_pre = false;
+};
+
+// obs (before the update), reward, goal / done update of agent i (navigation_graph_safe.py:
+// 606-875): sequential per agent in the reference, independent per lane here (the snapshot
+// rule is applied by the per-ego masks / rows afterwards).
+template <int DYN, int NT>
+__device__ __forceinline__ void reward_agent(const KParams& P, Lds& S, int env, int i, double mag, AgentTmp& t) {
+  LSM_DIMS;
+  write_obs<DYN, NT>(P, S, env, i);
+  const int gi = goal_index(S.rpre[i], i, N, NL);
+  const double gx = S.lm[gi], gy = S.lm[NL + gi], gh = S.lm[2 * NL + gi], gs = S.lm[3 * NL + gi];
+  const double px = S.ps[i], py = S.ps[N + i];
+  t.spd_pre = agent_speed<DYN>(S, N, i, false);
+  const double spd = t.spd_pre;
+  double he;
+  if (DYN == 0) {
+    // DI heading = atan2(vy, vx) (atan2(0, 0) = 0): its cos / sin are v / |v|, so
+    // direction_alignment_error = 0.5 - 0.5 cos(th - gh) needs no atan2 / cos (ulp-level
+    // vs the reference, like the integrator); goal sin / cos are cached per episode
+    if (spd > 0.0) {
+      const double inv = 1.0 / spd;
+      t.ct_pre = S.ps[2 * N + i] * inv;
+      t.st_pre = S.ps[3 * N + i] * inv;
+    }
+    he = 0.5 - 0.5 * (t.ct_pre * S.lmsc[NL + gi] + t.st_pre * S.lmsc[gi]);
+  } else {
+    t.th_pre = S.ps[2 * N + i];
+    he = dae(t.th_pre, gh);
+  }
+  const double th = t.th_pre;
+  const double hpr = 1 - np_clip(he / S.cur[C_GHE], 0, 1);
+  const double se = fabs(spd - gs);
+  const double sen = np_clip(se / S.cur[C_GSE], 0, 1);
+  const double cra = P.use_filter_arg ? 1.0 : S.cur[C_RAT];
+  const bool reached = goal_reached_at<DYN>(S, N, NL, i, gi, spd, he);
+  t.reached_pre = reached;
+  const bool done0 = S.dpre[i] != 0;
+  double r = 0.0;
+  if (reached) {
+    const double spr = 1 - sen;
+    const double ddx = gx - px, ddy = gy - py;
+    double cte = (DYN == 0) ? ddx * t.st_pre - ddy * t.ct_pre : ddx * sin(th) - ddy * cos(th);
+    cte = fabs(cte) / np_maximum(blas_norm2(ddx, ddy), 1e-6);
+    const double ctp = 1 - np_clip(cte, 0, 1);
+    const double perf = hpr * spr * ctp;
+    const double grew = (DYN == 0) ? 50 * perf : 50 * (perf * cra + (1 - cra));
+    if (!P.use_masking || !done0) r = r + grew;
+  }
+  if (!done0) {
+    if (DYN == 0) {
+      if (!P.use_filter_arg) {
+        double pen = 3 * mag;
+        pen = np_clip(1 - S.cur[C_SLOPED], 0, 1) * pen;
+        r = r - pen;
+      }
+      r = P.use_filter_arg ? r - 1.0 : r - 1.0 * S.cur[C_SLOPED];
+    } else {
+      double rpx, rpy;
+      blas_rot(S.lmsc[NL + gi], S.lmsc[gi], px - gx, py - gy, rpx, rpy);   // cached cos / sin(gh)
+      const double rs[4] = {rpx, rpy, th - gh, spd};
+      float ttr = 0.0f;
+      if (interp_value<4>(P.ttr, rs, ttr)) {
+        // reference: `rew -= 0.04 * ttr` with ttr a float32 (JAX) scalar: the product is
+        // float32; a python-int `rew` (no goal reward added) stays float32
+        const double ttrd = (double)(0.04f * ttr);
+        r = (reached && (!P.use_masking || !done0)) ? r - ttrd : (double)(float)(r - ttrd);
+      } else {
+        r = r - 0.04 * P.ttr_max;
+      }
+      r = r - sen * cra;
+    }
+  }
+  t.rew = np_clip(r, -40.0, 50.0);
+  int rp = S.rpre[i];
+  if (reached && (!P.use_masking || !done0)) rp += 1;
+  S.rpost[i] = rp;
+  S.dpost[i] = (rp >= L) ? 1 : S.dpre[i];
+  gptr(P.o.rew)[(size_t)env * N + i] = (float)t.rew;
+}
+
+// info_callback accumulators of agent i (navigation_graph_safe.py:386-450); `ncoll` = other
+// agents within the collision distance (is_collision, :497-501).
+template <int DYN, int NT>
+__device__ __forceinline__ void info_agent(const KParams& P, Lds& S, int i, int cstep, const AgentTmp& t,
+                                           int ncoll) {
+  LSM_DIMS;
+  const double tr_old = S.winfo[i], dg_old = S.winfo[N + i];
+  S.wold[i] = dg_old; S.wold[N + i] = tr_old;
+  double tr = tr_old, dg = dg_old, dl = S.winfo[2 * N + i];
+  const int gi = goal_index(S.rpost[i], i, N, NL);
+  const double dist = plain_norm2(S.ps[i] - S.lm[gi], S.ps[N + i] - S.lm[NL + gi]);
+  const double pd = S.pdist[i];
+  bool reached_post = t.reached_pre;   // same state and goal unless the goal advanced
+  if (S.rpost[i] != S.rpre[i]) {
+    const bool frz = S.dpost[i] != 0;
+    const double spp = frz ? 0.0 : t.spd_pre;
+    double hep;
+    if (DYN == 0) {   // frozen: zero velocity, atan2(0, 0) = 0
+      const double c = frz ? 1.0 : t.ct_pre, sn = frz ? 0.0 : t.st_pre;
+      hep = 0.5 - 0.5 * (c * S.lmsc[NL + gi] + sn * S.lmsc[gi]);
+    } else {
+      hep = dae(t.th_pre, S.lm[2 * NL + gi]);
+    }
+    reached_post = goal_reached_at<DYN>(S, N, NL, i, gi, spp, hep);
+  }
+  if (reached_post && tr == -1) {
+    tr = cstep * P.dt;
+    dg = pd;
+    dl = dist;
+  }
+  if (tr == -1) {
+    dg = pd;
+    dl = dist;
+  }
+  const double nc = S.winfo[3 * N + i] + (double)ncoll;   // is_collision count (:497-501)
+  S.winfo[i] = tr; S.winfo[N + i] = dg; S.winfo[2 * N + i] = dl; S.winfo[3 * N + i] = nc;
+  S.wnew[i] = dg; S.wnew[N + i] = tr;
+}
+
+// agent i's info row (LSM_INFO_FIELDS doubles at `inf`), after every agent's info_agent:
+// Distance / Time mean and std over the agents under the sequential snapshot rule.
+template <int NT>
+__device__ __forceinline__ void info_row(const KParams& P, const Lds& S, int i, double rew, double* inf) {
+  constexpr int DYN = 0;
+  LSM_DIMS;
+  struct Snap {
+    const double* nw;
+    const double* od;
+    int i;
+    __device__ double operator()(int j) const { return j <= i ? nw[j] : od[j]; }
+  };
+  double dm, ds, tm, ts;
+  np_mean_std(Snap{S.wnew, S.wold, i}, N, dm, ds);
+  np_mean_std(Snap{S.wnew + N, S.wold + N, i}, N, tm, ts);
+  const double mr = S.minrel[i];
+  inf[LSM_INFO_INDIVIDUAL_REWARD] = rew;
+  inf[LSM_INFO_MIN_RELATIVE_DISTANCE] = mr;
+  inf[LSM_INFO_DIST_TO_GOAL] = S.winfo[2 * N + i];
+  inf[LSM_INFO_TIME_REQ_TO_GOAL] = S.winfo[i];
+  inf[LSM_INFO_NUM_AGENT_COLLISIONS] = S.winfo[3 * N + i];
+  inf[LSM_INFO_DISTANCE_MEAN] = dm;
+  inf[LSM_INFO_DISTANCE_VARIANCE] = ds;
+  inf[LSM_INFO_DISTS_TRAVELED] = S.winfo[N + i];
+  inf[LSM_INFO_TIME_MEAN] = tm;
+  inf[LSM_INFO_TIME_STDDEV] = ts;
+  inf[LSM_INFO_MIN_TIME_TO_GOAL] = S.gmt[i];
+  inf[LSM_INFO_SAFETY_FILTERED] = (double)S.sfilt[i];
+  inf[LSM_INFO_SAFETY_VIOLATED] = (mr < S.cur[C_SEP]) ? 1.0 : 0.0;
+  inf[LSM_INFO_DECONFLICTING_INDEX] = (double)S.decon[i];
+  inf[LSM_INFO_ACTION_DIFF] = S.adiff[i];
+  inf[LSM_INFO_REACHED_GOAL] = (double)S.rpost[i];
+  inf[LSM_INFO_POSITION_X] = S.ps[i];
+  inf[LSM_INFO_POSITION_Y] = S.ps[N + i];
+}
+
+// Episode statistics of an active agent i (environment.py:1004-1022) from its neighbour
+// counts over the masked agent-agent distances: cnt in range, neng within the engagement
+// distance, mn the minimum.
+template <int DYN>
+__device__ __forceinline__ void stats_agent(const KParams& P, Lds& S, int N, int i, int cnt, int neng, double mn) {
+  S.stats[i] += 1;
+  double vx, vy;
+  agent_vel<DYN>(S, N, i, true, vx, vy);
+  S.stats[N + i] += blas_norm2(vx, vy) * P.dt;
+  if (cnt > 0) {
+    if (neng > 1) S.stats[5 * N + i] += 1;
+    if (mn < P.sep_target) S.stats[3 * N + i] += 1;
+    if (mn < S.stats[4 * N + i]) S.stats[4 * N + i] = mn;
+  }
 }
 
 template <int DYN, int LPE, int NT>
@@ -1475,53 +1868,7 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams* __restrict__
   STAMP(4);
 
   // ---- 4. integrate ----------------------------------------------------------------------
-  if (lane < N && !S.dpre[lane]) {
-    const int i = lane;
-    const double dt = P.dt;
-    const double a0 = S.safe[i], a1 = S.safe[N + i];
-    double x = S.ps[i], y = S.ps[N + i], s2 = S.ps[2 * N + i], s3 = S.ps[3 * N + i];
-    double spd;
-    if (DYN == 0) {
-      x = x + s2 * dt + 0.5 * a0 * dt * dt;
-      y = y + s3 * dt + 0.5 * a1 * dt * dt;
-      s2 = s2 + a0 * dt;
-      s3 = s3 + a1 * dt;
-      spd = sqrt(s2 * s2 + s3 * s3);
-      if (spd > P.max_speed) {
-        s2 = P.max_speed * s2 / spd;
-        s3 = P.max_speed * s3 / spd;
-      }
-      spd = sqrt(s2 * s2 + s3 * s3);
-    } else {
-      const double th0 = s2, v0 = s3, w = a0, ac = a1;
-      const double th1 = th0 + w * dt;
-      const double v1 = v0 + ac * dt;
-      // stable closed form about the mid-heading (oracle/lsm_oracle.py closed_form_step)
-      const double h = 0.5 * w * dt;
-      const double m = th0 + h;
-      const double cm = cos(m), sm = sin(m);
-      double sc, q;
-      if (fabs(h) < 0.1) {
-        const double h2 = h * h;
-        sc = 1.0 - h2 / 6.0 * (1.0 - h2 / 20.0 * (1.0 - h2 / 42.0 * (1.0 - h2 / 72.0)));
-        q = -h / 3.0 * (1.0 - h2 / 10.0 * (1.0 - h2 / 28.0 * (1.0 - h2 / 54.0)));
-      } else {
-        sc = sin(h) / h;
-        q = (cos(h) - sc) / h;
-      }
-      const double A = v0 * dt + 0.5 * ac * dt * dt;
-      const double B = 0.5 * ac * dt * dt;
-      x = x + (A * cm * sc + B * sm * q);
-      y = y + (A * sm * sc - B * cm * q);
-      s2 = th1;
-      s3 = v1;
-      if (s3 > P.max_speed) s3 = P.max_speed;
-      if (s3 < P.min_speed) s3 = P.min_speed;
-      spd = s3;
-    }
-    S.ps[i] = x; S.ps[N + i] = y; S.ps[2 * N + i] = s2; S.ps[3 * N + i] = s3;
-    S.pdist[i] += spd * dt;
-  }
+  if (lane < N && !S.dpre[lane]) integrate_agent<DYN>(P, S, N, lane);
   __syncthreads();
   STAMP(5);
 
@@ -1543,7 +1890,7 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams* __restrict__
   // ego's mask is the pre-update mask, so the adjacency can be stored now, in four chunks of
   // egos placed between the remaining phases: the stores drain while the wave computes
   // instead of queueing behind each other at the end. A status change rewrites it at the end.
-  const bool chunked = (E & 3) == 0;
+  const bool chunked = (E & 3) == 0 && !P.adj_compact;
   const uint64_t m_pre = chunked ? ego_mask(S, N, L, -1) : 0;
   if (chunked) emit_adj_uniform<LPE, NT>(P, S, env, m_pre, 0, N / 4);
   STAMP(6);
@@ -1551,82 +1898,9 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams* __restrict__
   // ---- 6. obs, reward, goal/done update ---------------------------------------------------
   double mag = 0.0;
   if (DYN == 0 && !P.use_filter_arg) mag = magnetic_penalty_wave<LPE, NT>(P, S, S.dpair);
-  double rew = 0.0;
-  double th_pre = 0.0, spd_pre = 0.0, ct_pre = 1.0, st_pre = 0.0;
-  bool reached_pre = false;
-  if (lane < N) {
-    const int i = lane;
-    write_obs<DYN, NT>(P, S, env, i);
-    const int gi = goal_index(S.rpre[i], i, N, NL);
-    const double gx = S.lm[gi], gy = S.lm[NL + gi], gh = S.lm[2 * NL + gi], gs = S.lm[3 * NL + gi];
-    const double px = S.ps[i], py = S.ps[N + i];
-    spd_pre = agent_speed<DYN>(S, N, i, false);
-    const double spd = spd_pre;
-    double he;
-    if (DYN == 0) {
-      // DI heading = atan2(vy, vx) (atan2(0, 0) = 0): its cos / sin are v / |v|, so
-      // direction_alignment_error = 0.5 - 0.5 cos(th - gh) needs no atan2 / cos (ulp-level
-      // vs the reference, like the integrator); goal sin / cos are cached per episode
-      if (spd > 0.0) {
-        const double inv = 1.0 / spd;
-        ct_pre = S.ps[2 * N + i] * inv;
-        st_pre = S.ps[3 * N + i] * inv;
-      }
-      he = 0.5 - 0.5 * (ct_pre * S.lmsc[NL + gi] + st_pre * S.lmsc[gi]);
-    } else {
-      th_pre = S.ps[2 * N + i];
-      he = dae(th_pre, gh);
-    }
-    const double th = th_pre;
-    const double hpr = 1 - np_clip(he / S.cur[C_GHE], 0, 1);
-    const double se = fabs(spd - gs);
-    const double sen = np_clip(se / S.cur[C_GSE], 0, 1);
-    const double cra = P.use_filter_arg ? 1.0 : S.cur[C_RAT];
-    const bool reached = goal_reached_at<DYN>(S, N, NL, i, gi, spd, he);
-    reached_pre = reached;
-    const bool done0 = S.dpre[i] != 0;
-    double r = 0.0;
-    if (reached) {
-      const double spr = 1 - sen;
-      const double ddx = gx - px, ddy = gy - py;
-      double cte = (DYN == 0) ? ddx * st_pre - ddy * ct_pre : ddx * sin(th) - ddy * cos(th);
-      cte = fabs(cte) / np_maximum(blas_norm2(ddx, ddy), 1e-6);
-      const double ctp = 1 - np_clip(cte, 0, 1);
-      const double perf = hpr * spr * ctp;
-      const double grew = (DYN == 0) ? 50 * perf : 50 * (perf * cra + (1 - cra));
-      if (!P.use_masking || !done0) r = r + grew;
-    }
-    if (!done0) {
-      if (DYN == 0) {
-        if (!P.use_filter_arg) {
-          double pen = 3 * mag;
-          pen = np_clip(1 - S.cur[C_SLOPED], 0, 1) * pen;
-          r = r - pen;
-        }
-        r = P.use_filter_arg ? r - 1.0 : r - 1.0 * S.cur[C_SLOPED];
-      } else {
-        double rpx, rpy;
-        blas_rot(S.lmsc[NL + gi], S.lmsc[gi], px - gx, py - gy, rpx, rpy);   // cached cos / sin(gh)
-        const double rs[4] = {rpx, rpy, th - gh, spd};
-        float ttr = 0.0f;
-        if (interp_value<4>(P.ttr, rs, ttr)) {
-          // reference: `rew -= 0.04 * ttr` with ttr a float32 (JAX) scalar: the product is
-          // float32; a python-int `rew` (no goal reward added) stays float32
-          const double ttrd = (double)(0.04f * ttr);
-          r = (reached && (!P.use_masking || !done0)) ? r - ttrd : (double)(float)(r - ttrd);
-        } else {
-          r = r - 0.04 * P.ttr_max;
-        }
-        r = r - sen * cra;
-      }
-    }
-    rew = np_clip(r, -40.0, 50.0);
-    int rp = S.rpre[i];
-    if (reached && (!P.use_masking || !done0)) rp += 1;
-    S.rpost[i] = rp;
-    S.dpost[i] = (rp >= L) ? 1 : S.dpre[i];
-    gptr(P.o.rew)[(size_t)env * N + i] = (float)rew;
-  }
+  AgentTmp at;
+  if (lane < N) reward_agent<DYN, NT>(P, S, env, lane, mag, at);
+  const double rew = at.rew;
   __syncthreads();
   if (lane < N) S.emask[lane] = ego_mask(S, N, L, lane);
   if (chunked) emit_adj_uniform<LPE, NT>(P, S, env, m_pre, N / 4, N / 2);
@@ -1634,76 +1908,13 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams* __restrict__
 
   // ---- 7/8. info_callback numbers -----------------------------------------------------
   if (lane < N) {
-    const int i = lane;
-    const double tr_old = S.winfo[i], dg_old = S.winfo[N + i];
-    S.wold[i] = dg_old; S.wold[N + i] = tr_old;
-    double tr = tr_old, dg = dg_old, dl = S.winfo[2 * N + i];
-    const int gi = goal_index(S.rpost[i], i, N, NL);
-    const double dist = plain_norm2(S.ps[i] - S.lm[gi], S.ps[N + i] - S.lm[NL + gi]);
-    const double pd = S.pdist[i];
-    bool reached_post = reached_pre;   // same state and goal unless the goal advanced
-    if (S.rpost[i] != S.rpre[i]) {
-      const bool frz = S.dpost[i] != 0;
-      const double spp = frz ? 0.0 : spd_pre;
-      double hep;
-      if (DYN == 0) {   // frozen: zero velocity, atan2(0, 0) = 0
-        const double c = frz ? 1.0 : ct_pre, sn = frz ? 0.0 : st_pre;
-        hep = 0.5 - 0.5 * (c * S.lmsc[NL + gi] + sn * S.lmsc[gi]);
-      } else {
-        hep = dae(th_pre, S.lm[2 * NL + gi]);
-      }
-      reached_post = goal_reached_at<DYN>(S, N, NL, i, gi, spp, hep);
-    }
-    if (reached_post && tr == -1) {
-      tr = cstep * P.dt;
-      dg = pd;
-      dl = dist;
-    }
-    if (tr == -1) {
-      dg = pd;
-      dl = dist;
-    }
-    double nc = S.winfo[3 * N + i];
-    for (int a = 0; a < N; ++a) {
-      if (a == i) continue;
-      if (S.aa2[i * N + a] < 1.05 * (0.05 + 0.05)) nc += 1;
-    }
-    S.winfo[i] = tr; S.winfo[N + i] = dg; S.winfo[2 * N + i] = dl; S.winfo[3 * N + i] = nc;
-    S.wnew[i] = dg; S.wnew[N + i] = tr;
+    int cc = 0;
+    for (int a = 0; a < N; ++a)
+      if (a != lane && S.aa2[lane * N + a] < 1.05 * (0.05 + 0.05)) cc++;
+    info_agent<DYN, NT>(P, S, lane, cstep, at, cc);
   }
   __syncthreads();
-  if (lane < N) {
-    const int i = lane;
-    struct Snap {
-      const double* nw;
-      const double* od;
-      int i;
-      __device__ double operator()(int j) const { return j <= i ? nw[j] : od[j]; }
-    };
-    double dm, ds, tm, ts;
-    np_mean_std(Snap{S.wnew, S.wold, i}, N, dm, ds);
-    np_mean_std(Snap{S.wnew + N, S.wold + N, i}, N, tm, ts);
-    double* inf = S.dpair + i * LSM_INFO_FIELDS;   // staged in U2 (filter scratch is dead)
-    const double mr = S.minrel[i];
-    inf[LSM_INFO_INDIVIDUAL_REWARD] = rew;
-    inf[LSM_INFO_MIN_RELATIVE_DISTANCE] = mr;
-    inf[LSM_INFO_DIST_TO_GOAL] = S.winfo[2 * N + i];
-    inf[LSM_INFO_TIME_REQ_TO_GOAL] = S.winfo[i];
-    inf[LSM_INFO_NUM_AGENT_COLLISIONS] = S.winfo[3 * N + i];
-    inf[LSM_INFO_DISTANCE_MEAN] = dm;
-    inf[LSM_INFO_DISTANCE_VARIANCE] = ds;
-    inf[LSM_INFO_DISTS_TRAVELED] = S.winfo[N + i];
-    inf[LSM_INFO_TIME_MEAN] = tm;
-    inf[LSM_INFO_TIME_STDDEV] = ts;
-    inf[LSM_INFO_MIN_TIME_TO_GOAL] = S.gmt[i];
-    inf[LSM_INFO_SAFETY_FILTERED] = (double)S.sfilt[i];
-    inf[LSM_INFO_SAFETY_VIOLATED] = (mr < S.cur[C_SEP]) ? 1.0 : 0.0;
-    inf[LSM_INFO_DECONFLICTING_INDEX] = (double)S.decon[i];
-    inf[LSM_INFO_ACTION_DIFF] = S.adiff[i];
-    inf[LSM_INFO_REACHED_GOAL] = (double)S.rpost[i];
-    inf[LSM_INFO_POSITION_X] = S.ps[i];
-    inf[LSM_INFO_POSITION_Y] = S.ps[N + i];
-  }
+  if (lane < N) info_row<NT>(P, S, lane, rew, S.dpair + lane * LSM_INFO_FIELDS);   // staged in U2
   __syncthreads();
   rec_copy<LPE>((const f32x4*)S.dpair, (GAS f32x4*)(gptr(P.o.info) + (size_t)env * N * LSM_INFO_FIELDS),
                 N * LSM_INFO_FIELDS / 2);
@@ -1715,10 +1926,6 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams* __restrict__
   if (lane < N) {
     const int i = lane;
     if (!S.dpost[i]) {  // departed is always True in the training scenario
-      S.stats[i] += 1;
-      double vx, vy;
-      agent_vel<DYN>(S, N, i, true, vx, vy);
-      S.stats[N + i] += blas_norm2(vx, vy) * P.dt;
       const uint64_t m = S.emask[i];
       int cnt = 0, neng = 0;
       double mn = INFINITY;
@@ -1730,11 +1937,7 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams* __restrict__
         if (d < P.world_eng) neng++;
         mn = (d < mn) ? d : mn;
       }
-      if (cnt > 0) {
-        if (neng > 1) S.stats[5 * N + i] += 1;
-        if (mn < P.sep_target) S.stats[3 * N + i] += 1;
-        if (mn < S.stats[4 * N + i]) S.stats[4 * N + i] = mn;
-      }
+      stats_agent<DYN>(P, S, N, i, cnt, neng, mn);
     }
     if (S.dpost[i]) S.stats[2 * N + i] = 1;
     my_done = S.dpost[i] || cstep >= P.episode_length;
@@ -1763,6 +1966,8 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams* __restrict__
   STAMP(11);
   RTSTAMP(14);
 }
+
+#include "lsm_block.h"
 
 // env k's MT19937: np.random.seed(seed + 1000 * (env_offset + k))
 __global__ void seed_kernel(uint32_t* mt, int n_envs, int64_t seed, int64_t env_offset) {
@@ -1797,6 +2002,7 @@ struct lsm_env {
   KParams* dparams;   // device copy of the per-handle constants (re-uploaded when dirty)
   bool params_dirty;
   int lpe;   // lanes per env
+  bool block;   // workgroup-per-env kernel (N > 32 or E > 64, or LSM_KERNEL=block)
   bool generic_only;   // LSM_GENERIC=1: never use the compile-time-N kernels (tests): 64 (one env per wave), 32 or 16 (2 or 4 envs per wave)
 };
 
@@ -1831,6 +2037,7 @@ static void fill_params(const lsm_env* e, KParams& P) {
   P.use_masking = e->cfg.use_masking;
   P.use_filter_arg = e->cfg.use_safety_filter;
   P.auto_reset = e->cfg.auto_reset;
+  P.adj_compact = e->cfg.adj_layout == LSM_ADJ_COMPACT;
   P.world_size = e->cfg.world_size;
   const double pi = 3.141592653589793;
   P.pi = pi;
@@ -1885,6 +2092,7 @@ static void fill_params(const lsm_env* e, KParams& P) {
   P.o.info = (double*)e->out_ptr[LSM_OUT_INFO];
   P.o.edges = (uint8_t*)e->out_ptr[LSM_OUT_EDGES];
   P.o.state = (double*)e->out_ptr[LSM_OUT_STATE];
+  P.o.adjmask = (uint64_t*)e->out_ptr[LSM_OUT_ADJ_MASK];
   P.stamps = (unsigned long long*)e->out_ptr[LSM_OUT_DEBUG_STAMPS];
   P.diag = 0;
 #ifdef LSM_STAMPS
@@ -1900,7 +2108,8 @@ size_t lsm_output_bytes(const lsm_env* e, int32_t slot) {
   switch (slot) {
     case LSM_OUT_OBS: return n * N * e->OBS * 4;
     case LSM_OUT_NODE_OBS: return n * N * E * e->F * 4;
-    case LSM_OUT_ADJ: return n * N * E * E * 4;
+    case LSM_OUT_ADJ: return (e->cfg.adj_layout == LSM_ADJ_COMPACT ? n : n * N) * E * E * 4;
+    case LSM_OUT_ADJ_MASK: return n * N * ((E + 63) / 64) * 8;
     case LSM_OUT_REWARD: return n * N * 4;
     case LSM_OUT_DONE: return n * N;
     case LSM_OUT_RESET_FLAG: return n;
@@ -1934,10 +2143,16 @@ int lsm_create(const lsm_config* cfg, lsm_env** out) {
   const int N = cfg->num_agents, L = cfg->num_landmarks;
   if (cfg->dynamics != LSM_DOUBLE_INTEGRATOR && cfg->dynamics != LSM_AIRTAXI)
     return fail(e, "dynamics must be LSM_DOUBLE_INTEGRATOR or LSM_AIRTAXI");
-  if (N < 2 || N > MAXN) return fail(e, "num_agents must be in [2, 32] for the one-wave kernel");
+  if (N < 2 || N > BMAXN) return fail(e, "num_agents must be in [2, 64]");
   if (L < 2 || L > MAX_L) return fail(e, "num_landmarks must be in [2, 8] (reference asserts > 1)");
-  if (N * (1 + L) > MAXE) return fail(e, "N * (1 + L) must be <= 64 for the one-wave kernel");
-  if (N * L > 127) return fail(e, "landmark ids go through np.int8 (navigation_graph_safe.py:581)");
+  if (N * (1 + L) > BMAXE) return fail(e, "N * (1 + L) must be <= 256");
+  if (N * L - 1 > 127) return fail(e, "landmark ids go through np.int8 (navigation_graph_safe.py:581)");
+  if (cfg->adj_layout != LSM_ADJ_REFERENCE && cfg->adj_layout != LSM_ADJ_COMPACT)
+    return fail(e, "adj_layout must be LSM_ADJ_REFERENCE or LSM_ADJ_COMPACT");
+  {
+    const char* kv = getenv("LSM_KERNEL");
+    e->block = N > MAXN || N * (1 + L) > MAXE || (kv && strcmp(kv, "block") == 0);
+  }
   if (cfg->num_envs < 1) return fail(e, "num_envs must be >= 1");
   if (cfg->episode_length < 1) return fail(e, "episode_length must be >= 1");
   e->N = N; e->L = L; e->NL = N * L; e->E = N * (1 + L);
@@ -1949,12 +2164,13 @@ int lsm_create(const lsm_config* cfg, lsm_env** out) {
   e->lpe = 64;
   if (const char* v = getenv("LSM_LPE")) e->lpe = atoi(v);
   e->generic_only = getenv("LSM_GENERIC") && atoi(getenv("LSM_GENERIC")) != 0;
-  if (!(e->lpe == 16 || e->lpe == 32 || e->lpe == 64) || e->lpe < N)
+  if (e->block) e->lpe = 64;   // LSM_LPE applies to the one-wave kernel only
+  if (!(e->lpe == 16 || e->lpe == 32 || e->lpe == 64) || e->lpe < (e->block ? 1 : N))
     return fail(e, "LSM_LPE must be 16, 32 or 64 and >= num_agents");
   HIPCHK(e, hipGetDevice(&e->device));
   const size_t n = cfg->num_envs;
   int r = 0;
-  const LdsPlan lp = lds_plan(N, e->NL, e->E, e->F);
+  const LdsPlan lp = lds_plan(N, e->NL, e->E, e->F, e->block);
   e->s.rec16 = (uint32_t)(lp.rec / 16);
   e->s.hot16 = (uint32_t)(lp.hot / 16);
   e->s.rec_stride16 = (uint32_t)(((lp.rec + 127) / 128) * 8);   // 128-B aligned records
@@ -2102,6 +2318,8 @@ static int check_ready(lsm_env* e, bool stepping) {
                      LSM_OUT_RESET_FLAG, LSM_OUT_EP_INFO, LSM_OUT_INFO};
   for (int s : req)
     if (!e->out_ptr[s]) return fail(e, "output slot " + std::to_string(s) + " not bound");
+  if (e->cfg.adj_layout == LSM_ADJ_COMPACT && !e->out_ptr[LSM_OUT_ADJ_MASK])
+    return fail(e, "compact adjacency layout needs LSM_OUT_ADJ_MASK bound");
   (void)stepping;
   return 0;
 }
@@ -2114,9 +2332,23 @@ static void launch_t(lsm_env* e, const KStep& L, size_t env_lds, hipStream_t st)
                      (const KParams*)e->dparams, L);
 }
 
+extern "C++" template <int DYN, int NT>
+static int launch_block_t(lsm_env* e, const KStep& L, size_t env_lds, hipStream_t st) {
+  static bool attr = false;   // LDS above the 64 KB default needs an explicit opt-in
+  if (!attr && env_lds > 65536) {
+    HIPCHK(e, hipFuncSetAttribute((const void*)rollout_block_kernel<DYN, NT>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)env_lds));
+    attr = true;
+  }
+  hipLaunchKernelGGL((rollout_block_kernel<DYN, NT>), dim3(e->cfg.num_envs), dim3(BT), env_lds, st,
+                     (const KParams*)e->dparams, L);
+  return 0;
+}
+
 static int launch(lsm_env* e, KStep& L, hipStream_t st) {
-  const size_t env_lds = lds_plan(e->N, e->NL, e->E, e->F).bytes;
-  if (env_lds * (WAVE / e->lpe) > 65536) return fail(e, "LDS footprint too large");
+  const size_t env_lds = lds_plan(e->N, e->NL, e->E, e->F, e->block).bytes;
+  if (e->block ? env_lds > 160 * 1024 : env_lds * (WAVE / e->lpe) > 65536)
+    return fail(e, "LDS footprint too large");
   if (e->params_dirty) {   // outputs / tables changed: refresh the device copy (stream-ordered)
     KParams P;
     fill_params(e, P);
@@ -2129,10 +2361,20 @@ static int launch(lsm_env* e, KStep& L, hipStream_t st) {
 #ifdef LSM_STAMPS
   if (const char* v = getenv("LSM_STOP_AFTER")) L.stop_after = atoi(v);
 #endif
+  const bool di = e->cfg.dynamics == LSM_DOUBLE_INTEGRATOR;
+  if (e->block) {
+    // workgroup per env; compile-time N = 64 (config 5) or the generic kernel
+    const bool spec64 = e->N == 64 && e->L == 2 && !e->generic_only;
+    int rc;
+    if (di) rc = spec64 ? launch_block_t<0, 64>(e, L, env_lds, st) : launch_block_t<0, 0>(e, L, env_lds, st);
+    else rc = spec64 ? launch_block_t<1, 64>(e, L, env_lds, st) : launch_block_t<1, 0>(e, L, env_lds, st);
+    if (rc) return rc;
+    HIPCHK(e, hipGetLastError());
+    return 0;
+  }
   // specialised kernels (compile-time N, L = 2, one env per wave) for the BASELINE agent
   // counts; everything else runs the generic kernel (runtime dims, LPE 64/32/16)
   const bool spec = e->lpe == 64 && e->L == 2 && !e->generic_only;
-  const bool di = e->cfg.dynamics == LSM_DOUBLE_INTEGRATOR;
   if (spec && di && e->N == 3) launch_t<0, 64, 3>(e, L, env_lds, st);
   else if (spec && di && e->N == 8) launch_t<0, 64, 8>(e, L, env_lds, st);
   else if (spec && !di && e->N == 3) launch_t<1, 64, 3>(e, L, env_lds, st);
@@ -2158,7 +2400,7 @@ int lsm_set_agent_state(lsm_env* e, int32_t env_index, const double* state, cons
   if (!e || !state) return 1;
   if (env_index < 0 || env_index >= e->cfg.num_envs) return fail(e, "env_index out of range");
   HIPCHK(e, hipStreamSynchronize((hipStream_t)stream));
-  const LdsPlan lp = lds_plan(e->N, e->NL, e->E, e->F);
+  const LdsPlan lp = lds_plan(e->N, e->NL, e->E, e->F, e->block);
   std::vector<unsigned char> rec(lp.rec);
   float4* dev = e->s.rec + (size_t)env_index * e->s.rec_stride16;
   HIPCHK(e, hipMemcpy(rec.data(), dev, lp.rec, hipMemcpyDeviceToHost));
@@ -2208,7 +2450,7 @@ int lsm_host_mt_uniforms(uint32_t seed, int32_t count, double lo, double hi, dou
 int lsm_host_scenario(const lsm_config* cfg, const lsm_curriculum* cur, uint32_t seed, double* agent_state,
                       double* landmarks) {
   const int N = cfg->num_agents, L = cfg->num_landmarks, NL = N * L;
-  if (N < 2 || N > MAXN || L < 2 || L > MAX_L) return 1;
+  if (N < 2 || N > BMAXN || L < 2 || L > MAX_L) return 1;
   HostMT m;
   m.seed(seed);
   ScenarioParams sp;

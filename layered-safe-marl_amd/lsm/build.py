@@ -13,6 +13,7 @@ CSRC = os.path.join(os.path.dirname(HERE), "csrc")
 SRC = os.path.join(CSRC, "lsm_rollout.hip")
 OUT = os.path.join(CSRC, "liblsm_rollout.so")
 DEPS = [SRC, os.path.join(CSRC, "lsm_numeric.h"), os.path.join(CSRC, "lsm_scenario.h"),
+        os.path.join(CSRC, "lsm_block.h"),
         os.path.join(os.path.dirname(os.path.dirname(HERE)), "include", "lsm_rollout.h")]
 
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

@@ -133,5 +133,5 @@ class EnvArgs:
             raise ValueError("num_env_steps // episode_length // n_rollout_threads == 0: the "
                              "reference's update_curriculum divides by it (navigation_graph_safe.py:326)")
         n_lm = self.num_agents * self.num_landmarks
-        if n_lm > 127:
+        if n_lm - 1 > 127:
             raise ValueError("landmark ids are addressed through np.int8 (navigation_graph_safe.py:581)")

@@ -21,21 +21,27 @@ as ``gather_bytes`` -- they are not HBM-algorithmic bytes.
 from __future__ import annotations
 
 
-def step_bytes(N: int, L: int = 2, dynamics: str = "double_integrator", filter_on: bool = True) -> dict:
+def step_bytes(N: int, L: int = 2, dynamics: str = "double_integrator", filter_on: bool = True,
+               adj_layout: str = "reference") -> dict:
+    """`adj_layout` "compact": one unmasked E x E f32 table per env + N * ceil(E/64) u64
+    masks instead of N * E * E f32. Envs with N > 32 or E > 64 run the workgroup kernel,
+    whose record has no landmark-pair cache."""
     NL = N * L
     E = N + NL
+    block = N > 32 or E > 64
     di = dynamics == "double_integrator"
     F = 10 if di else 11
     OBS = 7 if di else 6
     a16 = lambda x: (x + 15) // 16 * 16
     hot = (a16(8 * 4 * N) + a16(8 * 6 * N) + a16(8 * 4 * N) + 4 * a16(8 * N) + 4 * a16(4 * N) + 16)
-    rec = hot + a16(8 * 12) + a16(8 * 6 * NL) + a16(4 * (NL * (NL - 1) // 2))
+    rec = hot + a16(8 * 12) + a16(8 * 6 * NL) + (0 if block else a16(4 * (NL * (NL - 1) // 2)))
     state_r = rec + N * 4
     state_w = hot
-    outputs = N * OBS * 4 + N * E * F * 4 + N * E * E * 4 + N * 4 + N + 1 + N * 18 * 8 + 4 * N * 8
+    adj = E * E * 4 + N * ((E + 63) // 64) * 8 if adj_layout == "compact" else N * E * E * 4
+    outputs = N * OBS * 4 + N * E * F * 4 + adj + N * 4 + N + 1 + N * 18 * 8 + 4 * N * 8
     hbm = state_r + state_w + outputs
     corners = 16 if di else 32
     gw = 16 if di else 32
     gathers = (corners * 4 * N * (N - 1) + corners * gw * N) if filter_on else 0
     return dict(hbm_bytes=hbm, outputs=outputs, state=state_r + state_w, gather_bytes=gathers,
-                E=E, F=F, OBS=OBS)
+                E=E, F=F, OBS=OBS, block=block)

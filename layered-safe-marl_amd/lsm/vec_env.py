@@ -76,11 +76,23 @@ def infos_from_arrays(info, reset, ep_info, auto_reset=True):
     return tuple(out)
 
 
+def expand_compact_adj(adj, mask, E):
+    """adj[e][r][c] = (M[e] bit r | M[e] bit c) ? 0 : A[r][c] for the compact layout
+    (A: [n, E, E] float32, M: [n, N, W] int64 words of disconnect bits)."""
+    torch = _torch()
+    n, N, W = mask.shape
+    sh = torch.arange(64, device=mask.device, dtype=torch.int64)
+    bits = ((mask.unsqueeze(-1) >> sh) & 1).reshape(n, N, W * 64)[..., :E].bool()
+    keep = ~(bits.unsqueeze(-1) | bits.unsqueeze(-2))
+    return adj.unsqueeze(1) * keep
+
+
 class GpuGraphVecEnv:
     def __init__(self, all_args, num_envs: Optional[int] = None, device=None,
                  value_table: Optional[HjTable] = None, ttr_table: Optional[HjTable] = None,
                  auto_reset: bool = True, env_offset: int = 0, emit_edges: bool = False,
-                 return_numpy: bool = True, build_infos: bool = True, small_tables: bool = False):
+                 return_numpy: bool = True, build_infos: bool = True, small_tables: bool = False,
+                 adj_layout: str = "reference"):
         torch = _torch()
         self.args = EnvArgs.from_namespace(all_args) if not isinstance(all_args, EnvArgs) else all_args
         self.args.validate()
@@ -98,11 +110,16 @@ class GpuGraphVecEnv:
         self.build_infos = bool(build_infos)
         di = a.dynamics_type == "double_integrator"
         self.N = int(a.num_agents)
+        if adj_layout not in ("reference", "compact"):
+            raise ValueError("adj_layout must be 'reference' or 'compact'")
+        self.adj_layout = adj_layout
         cfg = capi.LsmConfig(dynamics=capi.LSM_DOUBLE_INTEGRATOR if di else capi.LSM_AIRTAXI,
                              num_envs=self.num_envs, num_agents=self.N, num_landmarks=int(a.num_landmarks),
                              episode_length=int(a.episode_length), use_safety_filter=int(bool(a.use_safety_filter)),
                              use_masking=int(bool(a.use_masking)), auto_reset=int(self.auto_reset),
-                             emit_edges=int(bool(emit_edges)), reserved0=0, world_size=float(a.world_size),
+                             emit_edges=int(bool(emit_edges)),
+                             adj_layout=capi.ADJ_COMPACT if adj_layout == "compact" else capi.ADJ_REFERENCE,
+                             world_size=float(a.world_size),
                              seed=int(a.seed), env_offset=int(env_offset))
         if int(a.seed) + 1000 * (int(env_offset) + self.num_envs - 1) >= 2 ** 32:
             raise ValueError("numpy seeds must be < 2**32 (seed + 1000 * env index)")
@@ -130,7 +147,13 @@ class GpuGraphVecEnv:
         dev = self.device
         self.t_obs = torch.zeros((n, N, self.OBS), dtype=torch.float32, device=dev)
         self.t_node = torch.zeros((n, N, E, F), dtype=torch.float32, device=dev)
-        self.t_adj = torch.zeros((n, N, E, E), dtype=torch.float32, device=dev)
+        if adj_layout == "compact":
+            # unmasked E x E table per env + per-ego disconnect bits (include/lsm_rollout.h)
+            self.t_adj = torch.zeros((n, E, E), dtype=torch.float32, device=dev)
+            self.t_adj_mask = torch.zeros((n, N, (E + 63) // 64), dtype=torch.int64, device=dev)
+        else:
+            self.t_adj = torch.zeros((n, N, E, E), dtype=torch.float32, device=dev)
+            self.t_adj_mask = None
         self.t_rew = torch.zeros((n, N), dtype=torch.float32, device=dev)
         self.t_done = torch.zeros((n, N), dtype=torch.bool, device=dev)   # u8 buffer, 0/1
         self.t_reset = torch.zeros((n,), dtype=torch.bool, device=dev)
@@ -142,7 +165,8 @@ class GpuGraphVecEnv:
                         (capi.OUT_ADJ, self.t_adj), (capi.OUT_REWARD, self.t_rew),
                         (capi.OUT_DONE, self.t_done), (capi.OUT_RESET_FLAG, self.t_reset),
                         (capi.OUT_EP_INFO, self.t_epinfo), (capi.OUT_INFO, self.t_info),
-                        (capi.OUT_STATE, self.t_state), (capi.OUT_EDGES, self.t_edges)):
+                        (capi.OUT_STATE, self.t_state), (capi.OUT_EDGES, self.t_edges),
+                        (capi.OUT_ADJ_MASK, self.t_adj_mask)):
             if t is None:
                 continue
             capi.check(self.lib.lsm_bind_output(h, slot, C.c_void_p(t.data_ptr()),
@@ -204,7 +228,7 @@ class GpuGraphVecEnv:
         ep = self._ep_info_all()
         if self.return_numpy:
             return (self.t_obs.cpu().numpy(), self.agent_id.cpu().numpy(), self.t_node.cpu().numpy(),
-                    self.t_adj.cpu().numpy(), ep)
+                    self.reference_adj().cpu().numpy(), ep)
         return self.t_obs, self.agent_id, self.t_node, self.t_adj, ep
 
     def _ep_info_all(self):
@@ -248,7 +272,7 @@ class GpuGraphVecEnv:
             return out + (0,) if not self.auto_reset else out
         obs = self.t_obs.cpu().numpy()
         node = self.t_node.cpu().numpy()
-        adj = self.t_adj.cpu().numpy()
+        adj = self.reference_adj().cpu().numpy()
         rew = self.t_rew.cpu().numpy()
         dones = self.t_done.cpu().numpy().astype(bool)
         infos = self._infos() if self.build_infos else None
@@ -265,6 +289,13 @@ class GpuGraphVecEnv:
         reset = self.t_reset.cpu().numpy()
         return infos_from_arrays(self.t_info.cpu().numpy(), reset,
                                  self.t_epinfo.cpu().numpy() if reset.any() else None, self.auto_reset)
+
+    def reference_adj(self):
+        """The adjacency in the reference layout [n, N, E, E] (device tensor). In the compact
+        layout it is expanded from the table and the per-ego masks (torch ops on the device)."""
+        if self.t_adj_mask is None:
+            return self.t_adj
+        return expand_compact_adj(self.t_adj, self.t_adj_mask, self.E)
 
     def set_agent_state(self, env_index: int, agent_state, reached=None):
         """Overwrite one env's agent states ([N][4]) and optionally reached_goal ([N])."""

@@ -62,7 +62,7 @@ def test_host_scenario_matches_oracle(lib, dyn, n, ep, filt):
     blk = curriculum.curriculum_block(args, ep)
     cfg = capi.LsmConfig(dynamics=0 if dyn == "double_integrator" else 1, num_envs=1, num_agents=n,
                          num_landmarks=2, episode_length=250, use_safety_filter=int(filt), use_masking=1,
-                         auto_reset=1, emit_edges=0, reserved0=0, world_size=ws, seed=seed, env_offset=0)
+                         auto_reset=1, emit_edges=0, adj_layout=0, world_size=ws, seed=seed, env_offset=0)
     st = np.zeros((n, 4))
     lm = np.zeros((2 * n, 4))
     cur = curriculum.to_struct(blk)

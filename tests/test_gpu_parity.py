@@ -30,10 +30,15 @@ def _info_col(name):
 GPU_FIXTURES = list(fixture_names())
 
 
+@pytest.mark.parametrize("kernel", ["wave", "block", "blockc"])
 @pytest.mark.parametrize("name", GPU_FIXTURES)
-def test_gpu_matches_reference_golden(name):
+def test_gpu_matches_reference_golden(name, kernel, monkeypatch):
+    """Every golden fixture through the one-wave kernel and the workgroup-per-env kernel
+    (LSM_KERNEL=block; "blockc": compact adjacency layout, expanded for the comparison)."""
+    if kernel != "wave":
+        monkeypatch.setenv("LSM_KERNEL", "block")
     z, meta = load(name)
-    env = _gpu_env(meta, emit_edges=True)
+    env = _gpu_env(meta, emit_edges=True, adj_layout="compact" if kernel == "blockc" else "reference")
     obs, aid, node, adj, ep = env.reset(meta["ep"])
     np.testing.assert_allclose(obs[0], z["reset0_obs"], rtol=0, atol=F32_ATOL)
     np.testing.assert_allclose(node[0], z["reset0_node"], rtol=0, atol=F32_ATOL)
@@ -109,12 +114,18 @@ CASES = [
 ]
 
 
-@pytest.mark.parametrize("lpe", [16, 32, 64, "64g"])
+@pytest.mark.parametrize("lpe", [16, 32, 64, "64g", "block", "blockc"])
 @pytest.mark.parametrize("case", range(len(CASES)))
 def test_gpu_matches_oracle_multi_env(case, lpe, monkeypatch):
     """16 (or 15: a partly filled last wave) envs with per-env seeds seed + 1000 k, random
-    actions, across an auto-reset; every kernel variant: 1, 2 or 4 envs/wave, and at one env
-    per wave both the compile-time-N kernel (N = 3, 8, 16) and the generic one ("64g")."""
+    actions, across an auto-reset; every kernel variant: 1, 2 or 4 envs/wave, at one env
+    per wave both the compile-time-N kernel (N = 3, 8, 16) and the generic one ("64g"), and
+    the workgroup-per-env kernel in both adjacency layouts ("block", "blockc")."""
+    layout = "reference"
+    if lpe in ("block", "blockc"):
+        monkeypatch.setenv("LSM_KERNEL", "block")
+        layout = "compact" if lpe == "blockc" else "reference"
+        lpe = 64
     if lpe == "64g":
         monkeypatch.setenv("LSM_GENERIC", "1")
         lpe = 64
@@ -124,7 +135,7 @@ def test_gpu_matches_oracle_multi_env(case, lpe, monkeypatch):
     meta = dict(num_landmarks=2, n_rollout_threads=1, use_masking=True, num_internal_step=1, seed=5,
                 env_seed=5, **c)
     n_envs, steps = (16 if lpe == 64 else 15), min(c["episode_length"] + 20, 120)
-    env = _gpu_env(meta, n_envs=n_envs, seed=5)
+    env = _gpu_env(meta, n_envs=n_envs, seed=5, adj_layout=layout)
     ora = _oracle_for(meta, 5, n_envs)
     g = env.reset(ep)
     o = ora.reset(ep)
@@ -189,6 +200,111 @@ def test_gpu_full_size_properties_and_sampled_oracle():
             r = o.step(a_h[k:k + 1], 4)
             np.testing.assert_array_equal(dones[k].cpu().numpy(), r[5][0], err_msg="env %d step %d" % (k, t))
             np.testing.assert_array_equal((adj[k] != 0).cpu().numpy(), r[3][0] != 0)
+            np.testing.assert_allclose(obs[k].cpu().numpy(), r[0][0], rtol=0, atol=F32_ATOL)
+            np.testing.assert_allclose(st[k].cpu().numpy(), o.envs[0].s, rtol=0, atol=STATE_ATOL)
+    env.close()
+
+
+LARGE_CASES = [
+    # BASELINE config 5's env (64 double-integrator agents, E = 192), filter on, short episodes
+    dict(dynamics_type="double_integrator", num_agents=64, world_size=4, episode_length=10,
+         num_env_steps=10 * 4, use_safety_filter=True, ep=4),
+    # filter off (magnetic-field penalty over 256 lanes), curriculum mid-way
+    dict(dynamics_type="double_integrator", num_agents=64, world_size=4, episode_length=10,
+         num_env_steps=10 * 4, use_safety_filter=False, ep=1),
+    # generic workgroup kernel: odd N, E = 99 (not a multiple of 4, two mask words)
+    dict(dynamics_type="double_integrator", num_agents=33, world_size=4, episode_length=10,
+         num_env_steps=10 * 4, use_safety_filter=True, ep=4),
+    # airtaxi with E = 120
+    dict(dynamics_type="airtaxi", num_agents=40, world_size=6, episode_length=10,
+         num_env_steps=10 * 4, use_safety_filter=True, ep=4),
+]
+
+
+@pytest.mark.parametrize("layout", ["compact", "reference"])
+@pytest.mark.parametrize("case", range(len(LARGE_CASES)))
+def test_gpu_large_n_matches_oracle(case, layout):
+    """N > 32 (the workgroup-per-env kernel, chosen automatically): 2 envs over 13 steps
+    (one auto-reset at step 10) vs the oracle, every output."""
+    c = dict(LARGE_CASES[case])
+    ep = c.pop("ep")
+    meta = dict(num_landmarks=2, n_rollout_threads=1, use_masking=True, num_internal_step=1, seed=11,
+                env_seed=11, **c)
+    n_envs, N = 2, meta["num_agents"]
+    env = _gpu_env(meta, n_envs=n_envs, seed=11, adj_layout=layout, emit_edges=True)
+    ora = _oracle_for(meta, 11, n_envs)
+    g = env.reset(ep)
+    o = ora.reset(ep)
+    np.testing.assert_allclose(g[0], o[0], rtol=0, atol=F32_ATOL)
+    np.testing.assert_allclose(g[2], o[2], rtol=0, atol=F32_ATOL)
+    np.testing.assert_allclose(g[3], o[3], rtol=0, atol=F32_ATOL)
+    np.testing.assert_array_equal(g[3] != 0, o[3] != 0)
+    rng = np.random.default_rng(100 + case)
+    for t in range(13):
+        a = rng.integers(0, 25, (n_envs, N))
+        g = env.step(a, ep)
+        o = ora.step(a, ep)
+        ctx = "case %d step %d" % (case, t)
+        np.testing.assert_array_equal(g[5], o[5], err_msg=ctx)
+        np.testing.assert_array_equal(g[3] != 0, o[3] != 0, err_msg=ctx)
+        np.testing.assert_allclose(g[0], o[0], rtol=0, atol=F32_ATOL, err_msg=ctx)
+        np.testing.assert_allclose(g[2], o[2], rtol=0, atol=F32_ATOL, err_msg=ctx)
+        np.testing.assert_allclose(g[3], o[3], rtol=0, atol=F32_ATOL, err_msg=ctx)
+        np.testing.assert_allclose(g[4], o[4], rtol=1e-6, atol=1e-5, err_msg=ctx)
+        st = env.state().cpu().numpy()
+        info = env.t_info.cpu().numpy()
+        for k, e in enumerate(ora.envs):
+            np.testing.assert_allclose(st[k], e.s, rtol=0, atol=STATE_ATOL, err_msg=ctx)
+        for k in range(n_envs):
+            for i in range(N):
+                oi = o[6][k][i]
+                for name in ("min_relative_distance", "Num_agent_collisions", "Dist_to_goal", "Distance_mean",
+                             "Time_mean"):
+                    np.testing.assert_allclose(info[k, i, _info_col(name)], oi[name], rtol=1e-9, atol=1e-9,
+                                               err_msg=ctx + " " + name)
+                assert bool(info[k, i, _info_col("Safety filtered")]) == bool(oi["Safety filtered"]), ctx
+            e = ora.envs[k]
+            if env.t_reset.cpu().numpy()[k]:
+                continue   # the oracle env's per-step arrays were re-initialised by its reset
+            np.testing.assert_array_equal(info[k, :, _info_col("deconflicting_agent_index")].astype(int),
+                                          e.deconflicting, err_msg=ctx)
+            np.testing.assert_allclose(info[k, :, _info_col("action_diff")], e.action_diff, rtol=0, atol=1e-12,
+                                       err_msg=ctx)
+    env.close()
+
+
+def test_gpu_config5_full_size_compact():
+    """BASELINE config 5's per-GPU shard (64 DI agents x 8192 envs, filter on, compact
+    adjacency): invariants over 12 steps + exact replay of sampled envs through the oracle."""
+    import torch
+    meta = dict(dynamics_type="double_integrator", num_agents=64, num_landmarks=2, world_size=4,
+                episode_length=250, num_env_steps=250 * 4, n_rollout_threads=1, use_safety_filter=True,
+                use_masking=True, num_internal_step=1, seed=0, env_seed=0)
+    n_envs, N, E = 8192, 64, 192
+    env = _gpu_env(meta, n_envs=n_envs, seed=0, return_numpy=False, adj_layout="compact")
+    sample = [0, 8191]
+    oras = [_oracle_for(meta, 0, 1, env_offset=k) for k in sample]
+    obs, aid, node, adj, ep = env.reset(4)
+    assert adj.shape == (n_envs, E, E) and env.t_adj_mask.shape == (n_envs, N, 3)
+    for k, o in zip(sample, oras):
+        r = o.reset(4)
+        np.testing.assert_allclose(obs[k].cpu().numpy(), r[0][0], rtol=0, atol=F32_ATOL)
+    gen = torch.Generator(device="cuda:0").manual_seed(0)
+    for t in range(12):
+        a = torch.randint(0, 25, (n_envs, N), device="cuda:0", generator=gen, dtype=torch.int32)
+        obs, aid, node, adj, rew, dones, (info, reset, epinfo) = env.step(a, 4)
+        assert torch.isfinite(obs).all() and torch.isfinite(node).all()
+        assert (adj >= 0).all() and (adj < 4).all() and torch.equal(adj, adj.transpose(1, 2))
+        assert (torch.diagonal(adj, dim1=1, dim2=2) == 0).all()
+        st = env.state()
+        assert (torch.sqrt(st[..., 2] ** 2 + st[..., 3] ** 2) <= 0.5 + 1e-12).all()
+        a_h = a.cpu().numpy()
+        ref_adj = env.reference_adj()
+        for k, o in zip(sample, oras):
+            r = o.step(a_h[k:k + 1], 4)
+            np.testing.assert_array_equal(dones[k].cpu().numpy(), r[5][0])
+            np.testing.assert_allclose(ref_adj[k].cpu().numpy(), r[3][0], rtol=0, atol=F32_ATOL)
+            np.testing.assert_allclose(node[k].cpu().numpy(), r[2][0], rtol=0, atol=F32_ATOL)
             np.testing.assert_allclose(obs[k].cpu().numpy(), r[0][0], rtol=0, atol=F32_ATOL)
             np.testing.assert_allclose(st[k].cpu().numpy(), o.envs[0].s, rtol=0, atol=STATE_ATOL)
     env.close()
