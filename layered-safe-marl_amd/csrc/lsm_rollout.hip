@@ -425,32 +425,47 @@ enum { C_CR = 0, C_SLOPED, C_STAIR, C_RAT, C_RSC, C_GHE, C_GSE, C_MDT, C_SEP, C_
 // ----------------------------------------------------------------------------------
 // Wave-cooperative MT19937 (numpy legacy stream); all lanes run the same scalar sequence.
 // ----------------------------------------------------------------------------------
-template <int LPE>
+// WSYNC: the generator is run by one wave of a larger workgroup (the workgroup-per-env
+// kernel's reset): its refill synchronises that wave only.
+template <int LPE, bool WSYNC = false>
 struct WaveRng {
   uint32_t* key;
   int pos;
+  __device__ __forceinline__ void sync() {
+    if (WSYNC) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    } else {
+      __syncthreads();
+    }
+  }
   __device__ __forceinline__ void gen() {
+    // chunks of C <= 64 lanes: phase B's element i reads the NEW key[i - 227], so a chunk
+    // must not span more than 227 elements (the workgroup kernel's 256 lanes would)
+    constexpr int C = LPE < 64 ? LPE : 64;
     const int lane = threadIdx.x & (LPE - 1);
+    const bool act = lane < C;
     // phase A: i in [0, 227) reads old key[i], key[i+1], key[i+397]
-    for (int base = 0; base < MT_N - MT_M; base += LPE) {
+    for (int base = 0; base < MT_N - MT_M; base += C) {
       int i = base + lane;
       uint32_t v = 0;
-      if (i < MT_N - MT_M) v = mt_twist1(key[i], key[i + 1], key[i + MT_M]);
-      __syncthreads();
-      if (i < MT_N - MT_M) key[i] = v;
-      __syncthreads();
+      if (act && i < MT_N - MT_M) v = mt_twist1(key[i], key[i + 1], key[i + MT_M]);
+      sync();
+      if (act && i < MT_N - MT_M) key[i] = v;
+      sync();
     }
     // phases B, C: i in [227, 623) reads new key[i-227]
-    for (int base = MT_N - MT_M; base < MT_N - 1; base += LPE) {
+    for (int base = MT_N - MT_M; base < MT_N - 1; base += C) {
       int i = base + lane;
       uint32_t v = 0;
-      if (i < MT_N - 1) v = mt_twist1(key[i], key[i + 1], key[i + (MT_M - MT_N)]);
-      __syncthreads();
-      if (i < MT_N - 1) key[i] = v;
-      __syncthreads();
+      if (act && i < MT_N - 1) v = mt_twist1(key[i], key[i + 1], key[i + (MT_M - MT_N)]);
+      sync();
+      if (act && i < MT_N - 1) key[i] = v;
+      sync();
     }
     if (lane == 0) key[MT_N - 1] = mt_twist1(key[MT_N - 1], key[0], key[MT_M - 1]);
-    __syncthreads();
+    sync();
     pos = 0;
   }
   __device__ __forceinline__ uint32_t next32() {
@@ -1424,18 +1439,31 @@ __device__ __forceinline__ void reset_core(const KParams& P, Lds& S, int env, co
   const GAS uint32_t* mtg = gptr(P.s.mt) + (size_t)env * MT_WORDS;
   for (int k = lane; k < MT_WORDS; k += LPE) S.mt[k] = mtg[k];
   __syncthreads();
-  WaveRng<LPE> rng;
-  rng.key = S.mt;
-  rng.pos = (int)S.mt[MT_N];
   ScenarioParams sp;
   sp.dyn = DYN; sp.N = N; sp.L = L; sp.world_size = P.world_size; sp.coordination_range = P.coord_range;
   sp.goal_speed_min = P.gs_min; sp.goal_speed_max = P.gs_max;
   sp.ratio_airtaxi = S.cur[C_RAT]; sp.ratio_scenario = S.cur[C_RSC]; sp.two_pi = P.two_pi; sp.pi = P.pi;
-  // every lane runs the identical draw sequence and stores the identical values
-  random_scenario(rng, sp, S.ps, S.lm, S.scen);
-  __syncthreads();
-  if (lane == 0) S.mt[MT_N] = (uint32_t)rng.pos;
-  __syncthreads();
+  if (LPE > WAVE) {
+    // workgroup kernel: the scenario's read-modify-writes of its LDS workspace are only safe
+    // when every writer runs in lockstep, so one wave draws it (the others wait below)
+    if ((int)threadIdx.x < WAVE) {
+      WaveRng<WAVE, true> rng;
+      rng.key = S.mt;
+      rng.pos = (int)S.mt[MT_N];
+      random_scenario(rng, sp, S.ps, S.lm, S.scen);
+      if (lane == 0) S.mt[MT_N] = (uint32_t)rng.pos;
+    }
+    __syncthreads();
+  } else {
+    WaveRng<LPE> rng;
+    rng.key = S.mt;
+    rng.pos = (int)S.mt[MT_N];
+    // every lane runs the identical draw sequence and stores the identical values
+    random_scenario(rng, sp, S.ps, S.lm, S.scen);
+    __syncthreads();
+    if (lane == 0) S.mt[MT_N] = (uint32_t)rng.pos;
+    __syncthreads();
+  }
   GAS uint32_t* mtw = gptr(P.s.mt) + (size_t)env * MT_WORDS;
   for (int k = lane; k < MT_WORDS; k += LPE) mtw[k] = S.mt[k];
   for (int k = lane; k < NL; k += LPE) {

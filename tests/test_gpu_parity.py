@@ -186,7 +186,7 @@ def test_gpu_full_size_properties_and_sampled_oracle():
         st = env.state()
         if t % 20 == 0 or t >= 248:
             assert torch.isfinite(obs).all() and torch.isfinite(node).all() and torch.isfinite(adj).all()
-            assert (adj >= 0).all() and (adj < 4).all()
+            assert (adj >= 0).all() and (adj <= 4).all()   # the float32 cast of d < 4 may be 4.0f
             d = torch.diagonal(adj, dim1=2, dim2=3)
             assert (d == 0).all()
             assert torch.equal(adj, adj.transpose(2, 3))
@@ -294,7 +294,8 @@ def test_gpu_config5_full_size_compact():
         a = torch.randint(0, 25, (n_envs, N), device="cuda:0", generator=gen, dtype=torch.int32)
         obs, aid, node, adj, rew, dones, (info, reset, epinfo) = env.step(a, 4)
         assert torch.isfinite(obs).all() and torch.isfinite(node).all()
-        assert (adj >= 0).all() and (adj < 4).all() and torch.equal(adj, adj.transpose(1, 2))
+        # d < 4 in float64; the float32 cast may round up to exactly 4.0f
+        assert (adj >= 0).all() and (adj <= 4).all() and torch.equal(adj, adj.transpose(1, 2))
         assert (torch.diagonal(adj, dim1=1, dim2=2) == 0).all()
         st = env.state()
         assert (torch.sqrt(st[..., 2] ** 2 + st[..., 3] ** 2) <= 0.5 + 1e-12).all()
