@@ -238,6 +238,11 @@ __global__ __launch_bounds__(BT) void rollout_block_kernel(const KParams* __rest
   __syncthreads();
 
   // ---- 3. safety filter: T threads per ego, butterfly argmins --------------------------------
+  // The argmin of the HJ value over the other active agents needs exact values only where it
+  // can be decided: pass 1 bounds every in-range pair by its block's (min, max) (an L2-resident
+  // table) and takes the smallest upper bound U over the ego's pairs; pass 2 looks up the exact
+  // value only where the lower bound is <= U. A skipped pair's value exceeds U >= the minimum,
+  // so the argmin (first occurrence on ties) and its value are exactly the full search's.
   const bool filter_on = S.cur[C_FILT] != 0.0;
   if (filter_on) {
     const int i = tid / TE, q = tid - (tid / TE) * TE;
@@ -245,29 +250,51 @@ __global__ __launch_bounds__(BT) void rollout_block_kernel(const KParams* __rest
     double dmin = 0.0;
     float vmin = 0.0f;
     const bool ego = i < N && !S.dpre[i];
+    float ub = INFINITY;
     if (ego) {
-#pragma unroll 1
+#pragma unroll 2
       for (int j = q; j < N; j += TE) {
         if (j == i || S.dpre[j]) continue;
         const double ex = S.ps[i], ey = S.ps[N + i], ox = S.ps[j], oy = S.ps[N + j];
         const double d = sqrt((ox - ex) * (ox - ex) + (oy - ey) * (oy - ey));
+        if (jd < 0 || d < dmin) { jd = j; dmin = d; }
         double rel[5];
         rel_state<DYN>(S, N, i, j, rel);
-        float v = 0.0f;
-        bool ok;
-        if (DYN == 0) ok = interp_value<4>(P.val, rel, v); else ok = interp_value<5>(P.val, rel, v);
-        if (!ok) v = INFINITY;
-        if (jd < 0 || d < dmin) { jd = j; dmin = d; }
+        float2 b;
+        if (DYN == 0 ? value_bounds<4>(P.val, rel, b) : value_bounds<5>(P.val, rel, b)) ub = fminf(ub, b.y);
+      }
+    }
+#pragma unroll
+    for (int off = 1; off < T; off <<= 1) {
+      if (off >= TE) break;
+      const int jd2 = __shfl_xor(jd, off);
+      const double d2 = __shfl_xor(dmin, off);
+      if (jd2 >= 0 && (jd < 0 || d2 < dmin || (d2 == dmin && jd2 < jd))) { jd = jd2; dmin = d2; }
+      ub = fminf(ub, __shfl_xor(ub, off));
+    }
+    if (ego) {
+#pragma unroll 1
+      for (int j = q; j < N; j += TE) {
+        if (j == i || S.dpre[j]) continue;
+        double rel[5];
+        rel_state<DYN>(S, N, i, j, rel);
+        float2 b;
+        const bool inr = DYN == 0 ? value_bounds<4>(P.val, rel, b) : value_bounds<5>(P.val, rel, b);
+        float v = INFINITY;
+        bool ok = false;
+        if (inr) {
+          if (b.x > ub) continue;   // cannot be the argmin
+          if (DYN == 0) ok = interp_value<4>(P.val, rel, v); else ok = interp_value<5>(P.val, rel, v);
+          if (!ok) v = INFINITY;
+        }
         if (jv < 0 || v < vmin) { jv = j; vmin = v; okv = ok ? 1 : 0; }
       }
     }
 #pragma unroll
     for (int off = 1; off < T; off <<= 1) {
       if (off >= TE) break;
-      const int jd2 = __shfl_xor(jd, off), jv2 = __shfl_xor(jv, off), ok2 = __shfl_xor(okv, off);
-      const double d2 = __shfl_xor(dmin, off);
+      const int jv2 = __shfl_xor(jv, off), ok2 = __shfl_xor(okv, off);
       const float v2 = __shfl_xor(vmin, off);
-      if (jd2 >= 0 && (jd < 0 || d2 < dmin || (d2 == dmin && jd2 < jd))) { jd = jd2; dmin = d2; }
       if (jv2 >= 0 && (jv < 0 || v2 < vmin || (v2 == vmin && jv2 < jv))) { jv = jv2; vmin = v2; okv = ok2; }
     }
     if (q == 0 && i < N) {

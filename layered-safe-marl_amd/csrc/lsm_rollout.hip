@@ -84,6 +84,12 @@ struct TableDev {
   float sp[5];
   int periodic[5];
   int gw;  // float4 per corner gradient (1 for <= 4 dims, 2 for 5 dims)
+  // Value bounds per block of 2^bshift cells per dim: (min, max) of the block's nodes widened
+  // by the fp32 interpolation error (bounds_kernel). Small enough to stay in L2; the
+  // workgroup kernel uses them to skip exact lookups that cannot be the argmin. nullptr: none.
+  const float2* bnd;
+  int bshift;
+  int bstride[5];   // blocks: stride per dim
 };
 
 // Persistent per-env state: ONE contiguous record per env (env-major, 128-B aligned
@@ -571,6 +577,71 @@ __device__ __forceinline__ void interp_grad(const TableDev& T, const double* s, 
 #pragma unroll
     for (int d = 0; d < ND; ++d) g[d] = g[d] + w[c] * gv[d];
   }
+}
+
+// Bounds of the interpolated value at s: the (widened) min / max of the block containing
+// its cell. Same in-range decision and cell index as grid_cell(); false = out of the grid
+// (the lookup is +inf, no load).
+template <int ND>
+__device__ __forceinline__ bool value_bounds(const TableDev& T, const double* s, float2& b) {
+  int blk = 0;
+#pragma unroll
+  for (int d = 0; d < ND; ++d) {
+    float sd = (float)s[d];
+    float p = (sd - T.lo[d]) / T.sp[d];
+    if (!(p == p) || fabsf(p) > 1.0e9f) return false;
+    const int n = T.n[d];
+    int f = (int)floorf(p);
+    if (T.periodic[d]) {
+      f = f % n;
+      if (f < 0) f += n;
+    } else {
+      if (p < 0.0f || p > (float)(n - 1)) return false;
+      if (f > n - 2) f = n - 2;
+    }
+    blk += (f >> T.bshift) * T.bstride[d];
+  }
+  b = gptr(T.bnd)[blk];
+  return true;
+}
+
+// One thread per bounds block: min / max over the nodes its cells interpolate (cells
+// [b B, (b + 1) B) per dim -> nodes [b B, (b + 1) B] clipped, wrapped on periodic dims),
+// widened by 4e-6 max|v|: the fp32 sum of 2^d weighted corners stays within ~20 ulp of
+// max|v| of the exact convex combination, so an interpolated value never leaves the bounds.
+__global__ void bounds_kernel(const float* values, float2* bnd, TableDev T, int nblocks) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= nblocks) return;
+  const int B = 1 << T.bshift;
+  int lo[5], cnt[5];
+  int rem = b;
+  for (int d = T.ndim - 1; d >= 0; --d) {
+    const int ncell = T.periodic[d] ? T.n[d] : T.n[d] - 1;
+    const int nb = (ncell + B - 1) / B;
+    const int bd = rem % nb;
+    rem /= nb;
+    lo[d] = bd * B;
+    const int hi_cell = min(lo[d] + B, ncell);   // cells [lo, hi_cell)
+    cnt[d] = hi_cell - lo[d] + 1;                // nodes lo .. hi_cell
+  }
+  float mn = INFINITY, mx = -INFINITY;
+  int idx[5] = {0, 0, 0, 0, 0};
+  for (;;) {
+    int64_t node = 0;
+    for (int d = 0; d < T.ndim; ++d) {
+      int i = lo[d] + idx[d];
+      if (T.periodic[d] && i >= T.n[d]) i -= T.n[d];
+      node = node * T.n[d] + i;
+    }
+    const float v = values[node];
+    mn = fminf(mn, v);
+    mx = fmaxf(mx, v);
+    int d = T.ndim - 1;
+    while (d >= 0 && ++idx[d] == cnt[d]) idx[d--] = 0;
+    if (d < 0) break;
+  }
+  const float m = 4.0e-6f * fmaxf(fabsf(mn), fabsf(mx));
+  bnd[b] = make_float2(mn - m, mx + m);
 }
 
 // Expand a node table into the cell-corner layout (one thread per (cell, corner)).
@@ -2309,12 +2380,38 @@ static int upload_table(lsm_env* e, TableDev& T, int32_t ndim, const double* lo,
   return 0;
 }
 
+// Value bounds per 4^ndim-cell block (TableDev::bnd), built from the node table.
+static int upload_bounds(lsm_env* e, TableDev& T, const float* values) {
+  T.bshift = 2;
+  const int B = 1 << T.bshift;
+  int nblocks = 1;
+  for (int d = T.ndim - 1; d >= 0; --d) {
+    const int ncell = T.periodic[d] ? T.n[d] : T.n[d] - 1;
+    T.bstride[d] = nblocks;
+    nblocks *= (ncell + B - 1) / B;
+  }
+  size_t nodes = 1;
+  for (int d = 0; d < T.ndim; ++d) nodes *= (size_t)T.n[d];
+  float* dv = nullptr;
+  HIPCHK(e, hipMalloc((void**)&dv, nodes * 4));
+  HIPCHK(e, hipMemcpy(dv, values, nodes * 4, hipMemcpyHostToDevice));
+  float2* bd = nullptr;
+  if (dalloc(e, &bd, (size_t)nblocks)) return 1;
+  hipLaunchKernelGGL(bounds_kernel, dim3((nblocks + 255) / 256), dim3(256), 0, 0, dv, bd, T, nblocks);
+  HIPCHK(e, hipGetLastError());
+  HIPCHK(e, hipDeviceSynchronize());
+  HIPCHK(e, hipFree(dv));
+  T.bnd = bd;
+  return 0;
+}
+
 int lsm_set_value_table(lsm_env* e, int32_t ndim, const double* lo, const double* hi, const int32_t* shape,
                         const int32_t* periodic, const float* values, const float* grads) {
   const int want = e->cfg.dynamics == LSM_DOUBLE_INTEGRATOR ? 4 : 5;
   if (ndim != want) return fail(e, "value table must be 4-D (double integrator) or 5-D (airtaxi)");
   if (!grads) return fail(e, "value table needs its gradient table");
   if (upload_table(e, e->val, ndim, lo, hi, shape, periodic, values, grads)) return 1;
+  if (upload_bounds(e, e->val, values)) return 1;
   e->tables_ok = (e->cfg.dynamics == LSM_DOUBLE_INTEGRATOR) || e->ttr.cells != nullptr;
   e->params_dirty = true;
   return 0;

@@ -19,7 +19,7 @@ import json
 import os
 import statistics
 
-KERNEL = "rollout_kernel"
+KERNEL = "rollout_kernel"   # the one-wave kernel; --kernel rollout_block_kernel for N > 32
 
 
 def _rows(d, suffix):
@@ -64,23 +64,25 @@ def main():
     t.add_argument("--config", type=int, required=True)
     t.add_argument("--envs", type=int, required=True)
     t.add_argument("--out", default=None)
+    t.add_argument("--kernel", default=KERNEL)
     c = sub.add_parser("counters")
     c.add_argument("dirs", nargs="+")
+    c.add_argument("--kernel", default=KERNEL)
     a = ap.parse_args()
     if a.cmd == "counters":
         for d in a.dirs:
             names = sorted({r["Counter_Name"] for r in _rows(d, "counter_collection.csv")})
             for n in names:
-                v, k = counter_per_launch(d, n)
+                v, k = counter_per_launch(d, n, a.kernel)
                 print("%-24s %16.1f  (mean of %d launches)" % (n, v, k))
         return
     if a.cmd == "stats":
         for r in kernel_stats(a.dir):
             print("%-80s %6d %10.2f us %6.2f%%" % (r["name"], r["calls"], r["avg_us"], r["pct"]))
         return
-    fetch_kib, nf = counter_per_launch(a.fetch_dir, "FETCH_SIZE")
-    write_kib, nw = counter_per_launch(a.write_dir, "WRITE_SIZE")
-    rec = {"num_envs": a.envs, "fetch_size_kib_raw": fetch_kib, "write_size_kib": write_kib,
+    fetch_kib, nf = counter_per_launch(a.fetch_dir, "FETCH_SIZE", a.kernel)
+    write_kib, nw = counter_per_launch(a.write_dir, "WRITE_SIZE", a.kernel)
+    rec = {"num_envs": a.envs, "kernel": a.kernel, "fetch_size_kib_raw": fetch_kib, "write_size_kib": write_kib,
            "fetch_bytes_corrected": 2 * fetch_kib * 1024, "write_bytes": write_kib * 1024,
            "hbm_bytes_per_launch": 2 * fetch_kib * 1024 + write_kib * 1024,
            "dispatches": [nf, nw],

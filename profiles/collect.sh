@@ -1,6 +1,6 @@
 #!/bin/bash
 # Profile collection for one round (run on the GPU box via gpurun, from the repo root):
-#   bash profiles/collect.sh r01 3
+#   bash profiles/collect.sh r01 3        (config 5: the workgroup kernel, rollout_block_kernel)
 # 1. rocprofv3 --kernel-trace --stats of the bench command (per-kernel durations);
 # 2. separate PMC passes (FETCH_SIZE, WRITE_SIZE, SQ instruction/stall counters) --
 #    never combined with any trace domain;
@@ -14,6 +14,8 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 BENCH="bench.py --config $CFG --steps 200 --warmup 20 --no-cpu-baseline"
 ENVS=$(python -c "import bench; print(bench.CONFIGS[$CFG]['envs'])")
+KERN=rollout_kernel
+if [ "$CFG" = "5" ]; then KERN=rollout_block_kernel; fi
 
 run() {  # run <name> <rocprofv3 args...>
   local name=$1; shift
@@ -30,8 +32,8 @@ run sq2 --pmc SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_AC
 cd "$ROOT/layered-safe-marl_amd"
 python -m lsm.pmc stats "$OUT/ktrace" > "$ROOT/profiles/${ROUND}_config${CFG}_kernel_stats.txt"
 cp "$(find "$OUT/ktrace" -name '*kernel_stats.csv' | head -n1)" "$ROOT/profiles/${ROUND}_config${CFG}_kernel_stats.csv"
-python -m lsm.pmc traffic "$OUT/fetch" "$OUT/write" --config "$CFG" --envs "$ENVS" \
+python -m lsm.pmc traffic "$OUT/fetch" "$OUT/write" --config "$CFG" --envs "$ENVS" --kernel "$KERN" \
     --out "$ROOT/profiles/pmc_traffic.json" > "$ROOT/profiles/${ROUND}_config${CFG}_traffic.json"
-python -m lsm.pmc counters "$OUT/sq1" "$OUT/sq2" > "$ROOT/profiles/${ROUND}_config${CFG}_sq_counters.txt"
+python -m lsm.pmc counters "$OUT/sq1" "$OUT/sq2" --kernel "$KERN" > "$ROOT/profiles/${ROUND}_config${CFG}_sq_counters.txt"
 cp "$ROOT/profiles/"${ROUND}_config${CFG}_* "$ROOT/profiles/pmc_traffic.json" "$ROOT/gpurun_out/"
 echo done
