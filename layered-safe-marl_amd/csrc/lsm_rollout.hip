@@ -601,7 +601,9 @@ __device__ __forceinline__ bool value_bounds(const TableDev& T, const double* s,
     }
     blk += (f >> T.bshift) * T.bstride[d];
   }
-  b = gptr(T.bnd)[blk];
+  typedef float f32x2 __attribute__((ext_vector_type(2)));
+  const f32x2 x = *((const GAS f32x2*)gptr(T.bnd) + blk);
+  b = make_float2(x.x, x.y);
   return true;
 }
 
