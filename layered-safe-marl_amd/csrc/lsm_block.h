@@ -183,12 +183,20 @@ __global__ __launch_bounds__(BT) void rollout_block_kernel(const KParams* __rest
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int env = blockIdx.x;
   const int tid = threadIdx.x;
+  const int lane = tid;   // (STAMP macros)
   if (env >= P.n_envs) return;   // uniform over the workgroup
   LSM_DIMS;
   const int MW = (E + 63) >> 6;
   constexpr int T = NT ? block_tpe(NT) : 64;      // butterfly bound (generic: up to 64 lanes)
   const int TE = NT ? T : block_tpe(N);           // threads per ego actually used
   Lds S = carve_block(smem, N, NL, E, F);
+  RTSTAMP(13);
+#ifdef LSM_STAMPS
+  if (tid == 0 && gptr(P.stamps))
+    gptr(P.stamps)[(size_t)env * 16 + 15] = (unsigned long long)__builtin_amdgcn_s_getreg(63492) |
+                                      ((unsigned long long)__builtin_amdgcn_s_getreg(6164) << 32);
+#endif
+  STAMP(0);
 
   // ---- 0. the env's record HBM -> LDS + this step's actions ------------------------------
   const int ai = (K.mode == 0 && tid < N) ? load_action(K, env, N, tid) : 0;
@@ -204,6 +212,7 @@ __global__ __launch_bounds__(BT) void rollout_block_kernel(const KParams* __rest
   }
   const int cstep = S.step[0] + 1;
   __syncthreads();
+  STAMP(1);
 
   if (K.mode == 1) {
     reset_block<DYN, NT>(P, S, env, K.cur_new);
@@ -236,6 +245,7 @@ __global__ __launch_bounds__(BT) void rollout_block_kernel(const KParams* __rest
     S.raw[N + tid] = P.act1[yi];
   }
   __syncthreads();
+  STAMP(2);
 
   // ---- 3. safety filter: T threads per ego, butterfly argmins --------------------------------
   // The argmin of the HJ value over the other active agents needs exact values only where it
@@ -250,53 +260,77 @@ __global__ __launch_bounds__(BT) void rollout_block_kernel(const KParams* __rest
     double dmin = 0.0;
     float vmin = 0.0f;
     const bool ego = i < N && !S.dpre[i];
-    float ub = INFINITY;
-    if (ego) {
-#pragma unroll 2
-      for (int j = q; j < N; j += TE) {
-        if (j == i || S.dpre[j]) continue;
-        const double ex = S.ps[i], ey = S.ps[N + i], ox = S.ps[j], oy = S.ps[N + j];
-        const double d = sqrt((ox - ex) * (ox - ex) + (oy - ey) * (oy - ey));
-        if (jd < 0 || d < dmin) { jd = j; dmin = d; }
-        double rel[5];
-        rel_state<DYN>(S, N, i, j, rel);
-        float2 b;
-        if (DYN == 0 ? value_bounds<4>(P.val, rel, b) : value_bounds<5>(P.val, rel, b)) ub = fminf(ub, b.y);
-      }
-    }
+    constexpr int JN = NT ? (NT + T - 1) / T : 0;   // pairs per thread (compile-time N)
+    if (JN > 0 && P.filter_search == 1) {
+      // pass 1: bounds of every pair, loads issued together (slots unrolled)
+      float lbk[JN > 0 ? JN : 1];   // +inf: no candidate; -inf: candidate outside the grid
+      float ub = INFINITY;
 #pragma unroll
-    for (int off = 1; off < T; off <<= 1) {
-      if (off >= TE) break;
-      const int jd2 = __shfl_xor(jd, off);
-      const double d2 = __shfl_xor(dmin, off);
-      if (jd2 >= 0 && (jd < 0 || d2 < dmin || (d2 == dmin && jd2 < jd))) { jd = jd2; dmin = d2; }
-      ub = fminf(ub, __shfl_xor(ub, off));
-    }
-    if (ego) {
-#pragma unroll 1
-      for (int j = q; j < N; j += TE) {
-        if (j == i || S.dpre[j]) continue;
-        double rel[5];
-        rel_state<DYN>(S, N, i, j, rel);
-        float2 b;
-        const bool inr = DYN == 0 ? value_bounds<4>(P.val, rel, b) : value_bounds<5>(P.val, rel, b);
+      for (int k = 0; k < JN; ++k) {
+        const int j = q + k * TE;
+        lbk[k] = INFINITY;
+        if (ego && j < N && j != i && !S.dpre[j]) {
+          const double ex = S.ps[i], ey = S.ps[N + i], ox = S.ps[j], oy = S.ps[N + j];
+          const double d = sqrt((ox - ex) * (ox - ex) + (oy - ey) * (oy - ey));
+          if (jd < 0 || d < dmin) { jd = j; dmin = d; }
+          double rel[5];
+          rel_state<DYN>(S, N, i, j, rel);
+          float2 b;
+          if (DYN == 0 ? value_bounds<4>(P.val, rel, b) : value_bounds<5>(P.val, rel, b)) {
+            lbk[k] = b.x;
+            ub = fminf(ub, b.y);
+          } else {
+            lbk[k] = -INFINITY;
+          }
+        }
+      }
+#pragma unroll
+      for (int off = 1; off < T; off <<= 1) ub = fminf(ub, __shfl_xor(ub, off));
+      // pass 2: exact values where the lower bound can still win
+#pragma unroll
+      for (int k = 0; k < JN; ++k) {
+        const float lb = lbk[k];
+        if (lb == INFINITY || lb > ub) continue;
+        const int j = q + k * TE;
         float v = INFINITY;
         bool ok = false;
-        if (inr) {
-          if (b.x > ub) continue;   // cannot be the argmin
+        if (lb != -INFINITY) {
+          double rel[5];
+          rel_state<DYN>(S, N, i, j, rel);
           if (DYN == 0) ok = interp_value<4>(P.val, rel, v); else ok = interp_value<5>(P.val, rel, v);
           if (!ok) v = INFINITY;
         }
         if (jv < 0 || v < vmin) { jv = j; vmin = v; okv = ok ? 1 : 0; }
       }
+    } else {
+      // full search: every pair's exact value (UNR lookups in flight per thread)
+      if (ego) {
+#pragma unroll 4
+        for (int j = q; j < N; j += TE) {
+          if (j == i || S.dpre[j]) continue;
+          const double ex = S.ps[i], ey = S.ps[N + i], ox = S.ps[j], oy = S.ps[N + j];
+          const double d = sqrt((ox - ex) * (ox - ex) + (oy - ey) * (oy - ey));
+          double rel[5];
+          rel_state<DYN>(S, N, i, j, rel);
+          float v = 0.0f;
+          bool ok;
+          if (DYN == 0) ok = interp_value<4>(P.val, rel, v); else ok = interp_value<5>(P.val, rel, v);
+          if (!ok) v = INFINITY;
+          if (jd < 0 || d < dmin) { jd = j; dmin = d; }
+          if (jv < 0 || v < vmin) { jv = j; vmin = v; okv = ok ? 1 : 0; }
+        }
+      }
     }
 #pragma unroll
     for (int off = 1; off < T; off <<= 1) {
       if (off >= TE) break;
-      const int jv2 = __shfl_xor(jv, off), ok2 = __shfl_xor(okv, off);
+      const int jd2 = __shfl_xor(jd, off), jv2 = __shfl_xor(jv, off), ok2 = __shfl_xor(okv, off);
+      const double d2 = __shfl_xor(dmin, off);
       const float v2 = __shfl_xor(vmin, off);
+      if (jd2 >= 0 && (jd < 0 || d2 < dmin || (d2 == dmin && jd2 < jd))) { jd = jd2; dmin = d2; }
       if (jv2 >= 0 && (jv < 0 || v2 < vmin || (v2 == vmin && jv2 < jv))) { jv = jv2; vmin = v2; okv = ok2; }
     }
+    STAMP(3);
     if (q == 0 && i < N) {
       double u0 = S.raw[i], u1 = S.raw[N + i];
       uint8_t fl = 0;
@@ -318,10 +352,12 @@ __global__ __launch_bounds__(BT) void rollout_block_kernel(const KParams* __rest
     S.adiff[tid] = blas_norm2(S.raw[tid] - u0, S.raw[N + tid] - u1);
   }
   __syncthreads();
+  STAMP(4);
 
   // ---- 4. integrate ------------------------------------------------------------------------
   if (tid < N && !S.dpre[tid]) integrate_agent<DYN>(P, S, N, tid);
   __syncthreads();
+  STAMP(5);
   entity_table<NT>(P, S);
 
   // ---- 5. min relative distance (active agents) and is_collision counts (all agents) ------
@@ -351,6 +387,7 @@ __global__ __launch_bounds__(BT) void rollout_block_kernel(const KParams* __rest
       S.ccnt[i] = cc;
     }
   }
+  STAMP(6);
 
   // ---- 6. obs, reward, goal/done update ---------------------------------------------------
   double mag = 0.0;
@@ -365,6 +402,7 @@ __global__ __launch_bounds__(BT) void rollout_block_kernel(const KParams* __rest
     const uint64_t sel = post_sel(N, L, e, w);
     S.emask[k] = (S.mpost[w] & sel) | (S.mpre[w] & ~sel);
   }
+  STAMP(7);
 
   // ---- 7/8. info_callback numbers -----------------------------------------------------------
   if (tid < N) info_agent<DYN, NT>(P, S, tid, cstep, at, S.ccnt[tid]);
@@ -373,6 +411,7 @@ __global__ __launch_bounds__(BT) void rollout_block_kernel(const KParams* __rest
   __syncthreads();
   rec_copy<BT>((const f32x4*)S.dpair, (GAS f32x4*)(gptr(P.o.info) + (size_t)env * N * LSM_INFO_FIELDS),
                N * LSM_INFO_FIELDS / 2);
+  STAMP(8);
 
   // ---- episode stats (environment.py:1004-1022), dones -------------------------------------
   {
@@ -411,6 +450,7 @@ __global__ __launch_bounds__(BT) void rollout_block_kernel(const KParams* __rest
     gptr(P.o.dones)[(size_t)env * N + tid] = my_done ? 1 : 0;
   }
   const bool all_done = __syncthreads_and(my_done);
+  STAMP(9);
 
   // ---- 9. graph outputs, or the auto-reset (whose outputs replace them) ---------------------
   if (tid == 0) { S.step[0] = cstep; S.step[1] = 0; }
@@ -423,6 +463,9 @@ __global__ __launch_bounds__(BT) void rollout_block_kernel(const KParams* __rest
     if (tid == 0) gptr(P.o.reset_flag)[env] = 0;
     emit_graph_block<DYN, NT>(P, S, env);
     __syncthreads();
+    STAMP(10);
     store_state<DYN, BT, NT>(P, S, smem, env, false);
   }
+  STAMP(11);
+  RTSTAMP(14);
 }

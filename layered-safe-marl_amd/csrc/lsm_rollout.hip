@@ -125,7 +125,9 @@ struct OutDev {
 struct KParams {
   int n_envs, N, L, NL, E, F, OBS, dyn, episode_length, use_masking, use_filter_arg, auto_reset;
   int adj_compact;   // LSM_ADJ_COMPACT: unmasked E x E table once per env + per-ego masks
+  int filter_search; // workgroup kernel's HJ argmin: 1 bound-pruned (default), 0 every pair exact
   double dt, world_size, coord_range, world_eng, sep_target, max_speed, min_speed, gs_min, gs_max;
+  double coord_range2;   // coord_range^2 (float64-rounded)
   double act0[5], act1[5];
   double mag_c[50], mag_s[50];
   double cos_pi6, two_pi, pi;
@@ -2139,6 +2141,8 @@ static void fill_params(const lsm_env* e, KParams& P) {
   P.use_filter_arg = e->cfg.use_safety_filter;
   P.auto_reset = e->cfg.auto_reset;
   P.adj_compact = e->cfg.adj_layout == LSM_ADJ_COMPACT;
+  P.filter_search = 1;
+  if (const char* v = getenv("LSM_FILTER_SEARCH")) P.filter_search = atoi(v);
   P.world_size = e->cfg.world_size;
   const double pi = 3.141592653589793;
   P.pi = pi;
@@ -2159,6 +2163,7 @@ static void fill_params(const lsm_env* e, KParams& P) {
       P.act1[k] = (k == 4) ? ahi : alo + k * ((ahi - alo) / 4);
     }
   }
+  P.coord_range2 = P.coord_range * P.coord_range;
   P.cos_pi6 = cos(pi / 6);
   for (int k = 0; k < 50; ++k) {
     const double ph = k * ((2 * pi - 0) / 50);   // np.linspace(0, 2pi, 50, endpoint=False)

@@ -51,7 +51,7 @@ def main():
                                                               c["dynamics_type"] != "double_integrator") else (None, None)
     n_envs = a.envs or c["envs"]
     env = GpuGraphVecEnv(args, num_envs=n_envs, device="cuda:0", value_table=vt, ttr_table=tt,
-                         return_numpy=False, build_infos=False)
+                         return_numpy=False, build_infos=False, adj_layout=c.get("adj_layout", "reference"))
     stamps = torch.zeros((n_envs, 16), dtype=torch.int64, device="cuda:0")
     capi.check(env.lib.lsm_bind_output(env.h, capi.OUT_DEBUG_STAMPS, C.c_void_p(stamps.data_ptr()),
                                        stamps.numel() * 8), env.h)
