@@ -286,20 +286,63 @@ __global__ __launch_bounds__(BT) void rollout_block_kernel(const KParams* __rest
       }
 #pragma unroll
       for (int off = 1; off < T; off <<= 1) ub = fminf(ub, __shfl_xor(ub, off));
-      // pass 2: exact values where the lower bound can still win
+      // pass 2: exact values where the lower bound can still win. The survivors of the wave's
+      // 64 lanes are compacted into a per-wave LDS queue (in U1, free during the filter) and
+      // looked up 64 at a time, so the gathers of different slots overlap instead of running
+      // one slot after another; each lane then walks its slots in order for the argmin.
+      uint32_t smask = 0;
+#pragma unroll
+      for (int k = 0; k < JN; ++k)
+        if (lbk[k] != INFINITY && lbk[k] != -INFINITY && !(lbk[k] > ub)) smask |= 1u << k;
+      const int wl = tid & (WAVE - 1);
+      const int cnt = __popc(smask);
+      int incl = cnt;
+#pragma unroll
+      for (int o = 1; o < WAVE; o <<= 1) {
+        const int y = __shfl_up(incl, o);
+        if (wl >= o) incl += y;
+      }
+      const int total = __shfl(incl, WAVE - 1);
+      const int base = incl - cnt;
+      uint16_t* qij = (uint16_t*)S.feat + (tid / WAVE) * (WAVE * JN);
+      float* qv = (float*)((uint16_t*)S.feat + (BT / WAVE) * (WAVE * JN)) + (tid / WAVE) * (WAVE * JN);
+      {
+        int p = base;
+        uint32_t m = smask;
+        while (m) {
+          const int k = __ffs(m) - 1;
+          m &= m - 1;
+          qij[p++] = (uint16_t)(i | ((q + k * TE) << 8));
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      for (int x = wl; x < total; x += WAVE) {
+        const int ii = qij[x] & 0xff, jj = qij[x] >> 8;
+        double rel[5];
+        rel_state<DYN>(S, N, ii, jj, rel);
+        float v = 0.0f;
+        const bool ok = DYN == 0 ? interp_value<4>(P.val, rel, v) : interp_value<5>(P.val, rel, v);
+        qv[x] = ok ? v : __builtin_nanf("");
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      int p = base;
 #pragma unroll
       for (int k = 0; k < JN; ++k) {
         const float lb = lbk[k];
-        if (lb == INFINITY || lb > ub) continue;
-        const int j = q + k * TE;
+        if (lb == INFINITY) continue;   // no candidate
         float v = INFINITY;
         bool ok = false;
         if (lb != -INFINITY) {
-          double rel[5];
-          rel_state<DYN>(S, N, i, j, rel);
-          if (DYN == 0) ok = interp_value<4>(P.val, rel, v); else ok = interp_value<5>(P.val, rel, v);
-          if (!ok) v = INFINITY;
+          if (lb > ub) continue;        // cannot be the argmin
+          const float r = qv[p++];
+          ok = !(r != r);
+          v = ok ? r : INFINITY;
         }
+        const int j = q + k * TE;
         if (jv < 0 || v < vmin) { jv = j; vmin = v; okv = ok ? 1 : 0; }
       }
     } else {

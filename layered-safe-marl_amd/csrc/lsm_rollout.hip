@@ -300,6 +300,10 @@ __host__ __device__ inline LdsPlan lds_plan(int N, int NL, int E, int F, bool bl
     m = m > (size_t)(8 * LSM_INFO_FIELDS * N) ? m : (size_t)(8 * LSM_INFO_FIELDS * N);
     size_t u1sz = e > g2 ? e : g2;
     u1sz = u1sz > align16(m) ? u1sz : align16(m);
+    // the filter's per-wave survivor queues (lsm_block.h): (i, j) u16 + value f32 per slot
+    const int tpe = (64 * N <= BT) ? 64 : (32 * N <= BT) ? 32 : (16 * N <= BT) ? 16 : (8 * N <= BT) ? 8 : 4;
+    const size_t qb = align16((size_t)(BT / WAVE) * WAVE * ((N + tpe - 1) / tpe) * 6);
+    u1sz = u1sz > qb ? u1sz : qb;
     p.off[k++] = u1; p.off[k++] = u1 + c; p.off[k++] = u1 + d;   // mt, scen, scratch
     p.off[k++] = u1; p.off[k++] = u1 + g1;                         // feat, egooff
     p.off[k++] = u1;                                               // dpair: pair partials / info rows
@@ -2389,7 +2393,8 @@ static int upload_table(lsm_env* e, TableDev& T, int32_t ndim, const double* lo,
 
 // Value bounds per 4^ndim-cell block (TableDev::bnd), built from the node table.
 static int upload_bounds(lsm_env* e, TableDev& T, const float* values) {
-  T.bshift = 2;
+  T.bshift = 2;   // 4 cells per dim: 180 KB for the full DI table (L2-resident)
+  if (const char* v = getenv("LSM_BOUNDS_SHIFT")) T.bshift = atoi(v);
   const int B = 1 << T.bshift;
   int nblocks = 1;
   for (int d = T.ndim - 1; d >= 0; --d) {
