@@ -108,6 +108,43 @@ def load_traffic(config, n_envs):
     return None
 
 
+def bench_edges(env, dev, reps=50):
+    """process_adj (count + scan + emit) over this GPU's n*N per-ego graphs of the last step.
+    Algorithmic bytes: the adjacency read twice (count and emit passes; compact: the table once per
+    ego graph + its mask words) + offsets + 16 B edge_index + 4 B edge_attr per edge."""
+    import torch
+    from lsm import edges
+    E, N = env.E, env.N
+    # at config 5 all 8192 x 64 per-ego graphs would be ~12 G edges (200 GiB): time the envs whose
+    # worst-case edge list fits 16 GiB, as a learner consuming minibatches would
+    m = max(1, min(env.num_envs, (16 << 30) // (N * E * E * 20)))
+    if env.t_adj_mask is None:
+        call = lambda: edges.process_adj(env.t_adj[:m].reshape(-1, E, E))
+    else:
+        call = lambda: edges.process_adj_compact(env.t_adj[:m], env.t_adj_mask[:m], N)
+    ei, ea = call()                                 # warm-up, allocates, loads kernels
+    nnz = ei.shape[1]
+    del ei, ea
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        call()
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps                 # includes the nnz host read-back per call
+    B = m * N
+    W = (E + 63) // 64
+    read = 2 * B * (E * E * 4 + (W * 8 if env.t_adj_mask is not None else 0))
+    written = nnz * 20 + (B + 1) * 8 + B * 8
+    gbps = (read + written) / (ms * 1e-3) / 1e9
+    return {"op": "GNNBase.process_adj (gnn.py:376-407) on the device", "envs": m, "graphs": B, "E": E,
+            "nnz": nnz, "ms_per_call": ms, "algorithmic_bytes": read + written, "achieved_GBps": gbps,
+            "frac_hbm_peak": gbps / PEAK_HBM_GBPS, "note": "two kernels + hipcub scan + one 8-B D2H read "
+            "of nnz per call (the torch.nonzero sync); re-reads of the adjacency in the emit pass are "
+            "L2/MALL hits"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -117,6 +154,9 @@ def main():
     ap.add_argument("--envs", type=int, default=0, help="envs per GPU (default: config's)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-cores", type=int, default=0)
+    ap.add_argument("--edges", action="store_true",
+                    help="also time GNNBase.process_adj (lsm_edges.hip) on the final adjacency and add an "
+                         "'edges' object to the JSON line (SURVEY 8(f) row 2; not part of the step)")
     a = ap.parse_args()
 
     from lsm.dist import rank_info, global_episode_summary
@@ -214,6 +254,8 @@ def main():
                          "gather_bytes_per_launch": sb["gather_bytes"] * n_envs},
             "cpu_baseline": cpu,
         }
+        if a.edges:
+            line["edges"] = bench_edges(env, dev)
         print(json.dumps(line), flush=True)
     env.close()
     if world > 1:

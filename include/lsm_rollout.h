@@ -151,6 +151,25 @@ int lsm_host_mt_uniforms(uint32_t seed, int32_t count, double lo, double hi, dou
 int lsm_host_scenario(const lsm_config* cfg, const lsm_curriculum* cur, uint32_t seed,
                       double* agent_state /* [N][4] */, double* landmarks /* [NL][4] */);
 
+/* ---- Learner hand-off: GNNBase.process_adj on the device (lsm_edges.hip) ------------------
+ * Replaces onpolicy/algorithms/utils/gnn.py:376-407 (GNNBase.process_adj): B adjacency matrices
+ * [B][E][E] -> edge_index int64 [2][nnz] (b*E + r, b*E + c) and edge_attr float32 [nnz][1], in
+ * nonzero() (row-major) order. `masks` == NULL: `adj` is the reference layout [B][E][E] (B = n*N
+ * per-ego graphs, or any batch). `masks` != NULL: the compact layout, `adj` = A [B/N][E][E] and
+ * `masks` = [B][ceil(E/64)] (LSM_OUT_ADJ / LSM_OUT_ADJ_MASK of an LSM_ADJ_COMPACT handle); the
+ * per-ego matrix is expanded on the fly. Two calls, like torch.nonzero's count-then-fill:
+ *   lsm_edges_count  offsets int64 [B+1] (offsets[B] = nnz), device; needs a device workspace of
+ *                    lsm_edges_workspace_bytes(B) bytes
+ *   lsm_edges_emit   fills edge_index / edge_attr given nnz (= offsets[B], read by the caller)
+ * Errors: nonzero return, text in lsm_edges_last_error() (per host thread). */
+size_t lsm_edges_workspace_bytes(int64_t B);
+int lsm_edges_count(const float* adj, const uint64_t* masks, int64_t B, int32_t E, int32_t N,
+                    int64_t* offsets, void* workspace, size_t workspace_bytes, void* hip_stream);
+int lsm_edges_emit(const float* adj, const uint64_t* masks, int64_t B, int32_t E, int32_t N,
+                   const int64_t* offsets, int64_t nnz, int64_t* edge_index, float* edge_attr,
+                   void* hip_stream);
+const char* lsm_edges_last_error(void);
+
 #ifdef __cplusplus
 }
 #endif

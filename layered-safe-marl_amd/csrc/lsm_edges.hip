@@ -1,0 +1,190 @@
+// lsm_edges.hip -- device-side GNNBase.process_adj: dense per-ego adjacency -> (edge_index, edge_attr).
+//
+// Reference: onpolicy/algorithms/utils/gnn.py:376-407 (GNNBase.process_adj). For a batch of B
+// adjacency matrices adj[B][E][E] the reference computes
+//     idx        = adj.nonzero()                       (row-major order over (b, r, c))
+//     edge_attr  = adj[idx[:,0], idx[:,1], idx[:,2]].unsqueeze(1)        float [nnz][1]
+//     edge_index = stack([b*E + r, b*E + c])                             int64 [2][nnz]
+// and the 2-D case (B = 1) is the same thing with b = 0. SURVEY §8(f) row 2: emit the learner's
+// graph input straight from the rollout's device buffers instead of the dense (n, N, E, E) tensor.
+//
+// Two adjacency sources:
+//   reference layout  adj[b][r][c]                     (LSM_ADJ_REFERENCE, b = env*N + ego)
+//   compact layout    A[env][r][c] + M[env][ego][W]    (LSM_ADJ_COMPACT): the reference value is
+//                     (M bit r | M bit c) ? 0 : A[r][c]; expanded on the fly, never materialised.
+//
+// Three launches, all HBM/L2-streaming integer work (no MFMA):
+//   edge_count_kernel   one wave per graph: nonzero count via 64-lane ballots -> counts[b]
+//   scan (hipcub)       inclusive sum of counts -> offsets[1..B], offsets[0] = 0, offsets[B] = nnz
+//   edge_emit_kernel    one wave per graph: re-reads its E*E values (L2 / MALL resident after the
+//                       count pass) and writes its edges at offsets[b] in row-major order; the
+//                       in-chunk position is the popcount of the ballot below the lane (mbcnt), so
+//                       the output order is exactly nonzero()'s.
+// A graph's E*E values are walked as one flat index k = r*E + c in 64-element chunks, so every
+// lane is busy whatever E is (E = 24 rows would leave 40 of 64 lanes idle per row).
+#include <hip/hip_runtime.h>
+#include <hipcub/device/device_scan.hpp>
+
+#include <cstdint>
+
+namespace {
+
+constexpr int WAVE = 64;
+constexpr int GRAPHS_PER_BLOCK = 4;   // 256-thread workgroups, one wave per graph
+
+struct AdjSrc {
+  const float* adj;         // reference: [B][E][E]; compact: [B / N][E][E]
+  const uint64_t* masks;    // compact only: [B][W] (== [n][N][W]); nullptr for reference
+  int64_t B;
+  int32_t E, N, W;
+  float inv_e;              // 1 / E for the flat-index row split
+};
+
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+
+// Row of flat index k (< E*E <= 65536): floor((k + 0.5) / E) in fp32 is exact here -- the
+// distance of (k + 0.5) / E from an integer is >= 0.5 / E >= 1/512, far above fp32 rounding.
+__device__ __forceinline__ int row_of(int k, float inv_e) { return (int)(((float)k + 0.5f) * inv_e); }
+
+__device__ __forceinline__ bool masked(const uint64_t* m, int r, int c) {
+  return ((m[r >> 6] >> (r & 63)) & 1ull) | ((m[c >> 6] >> (c & 63)) & 1ull);
+}
+
+// Value of element k of graph b (0 where masked in the compact layout).
+__device__ __forceinline__ float load_val(const AdjSrc& s, int64_t b, const float* g, const uint64_t* m,
+                                          int k) {
+  const float v = __builtin_nontemporal_load(g + k);
+  if (m == nullptr) return v;
+  const int r = row_of(k, s.inv_e);
+  const int c = k - r * s.E;
+  return masked(m, r, c) ? 0.0f : v;
+}
+
+__device__ __forceinline__ const float* graph_ptr(const AdjSrc& s, int64_t b) {
+  const int64_t EE = (int64_t)s.E * s.E;
+  return s.adj + (s.masks ? (b / s.N) : b) * EE;
+}
+
+__global__ __launch_bounds__(256) void edge_count_kernel(AdjSrc s, int64_t* __restrict__ counts) {
+  const int64_t b = (int64_t)blockIdx.x * GRAPHS_PER_BLOCK + (threadIdx.x >> 6);
+  if (b >= s.B) return;   // whole wave exits together
+  const float* g = graph_ptr(s, b);
+  const uint64_t* m = s.masks ? s.masks + b * s.W : nullptr;
+  const int EE = s.E * s.E;
+  int cnt = 0;
+  for (int k0 = 0; k0 < EE; k0 += WAVE) {
+    const int k = k0 + lane_id();
+    const bool nz = k < EE && load_val(s, b, g, m, k) != 0.0f;   // NaN counts, -0.0 does not (torch)
+    cnt += __popcll(__ballot(nz));
+  }
+  if (lane_id() == 0) counts[b] = cnt;
+}
+
+__global__ __launch_bounds__(256) void edge_emit_kernel(AdjSrc s, const int64_t* __restrict__ offsets,
+                                                        int64_t nnz, int64_t* __restrict__ edge_index,
+                                                        float* __restrict__ edge_attr) {
+  const int64_t b = (int64_t)blockIdx.x * GRAPHS_PER_BLOCK + (threadIdx.x >> 6);
+  if (b >= s.B) return;
+  const float* g = graph_ptr(s, b);
+  const uint64_t* m = s.masks ? s.masks + b * s.W : nullptr;
+  const int EE = s.E * s.E;
+  const int64_t node0 = b * s.E;
+  int64_t pos = offsets[b];
+  const int64_t end = offsets[b + 1];
+  if (end > nnz) return;   // caller's nnz is stale: write nothing rather than out of bounds
+  for (int k0 = 0; k0 < EE && pos < end; k0 += WAVE) {
+    const int k = k0 + lane_id();
+    const float v = k < EE ? load_val(s, b, g, m, k) : 0.0f;
+    const bool nz = v != 0.0f;
+    const uint64_t bal = __ballot(nz);
+    if (nz) {
+      const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+      const int64_t o = pos + below;
+      const int r = row_of(k, s.inv_e);
+      edge_index[o] = node0 + r;
+      edge_index[nnz + o] = node0 + (k - r * s.E);
+      edge_attr[o] = v;
+    }
+    pos += __popcll(bal);
+  }
+}
+
+__global__ void zero_first(int64_t* offsets) { offsets[0] = 0; }
+
+thread_local char g_err[256];
+
+int fail(const char* msg) {
+  snprintf(g_err, sizeof g_err, "%s", msg);
+  return 1;
+}
+
+int make_src(const float* adj, const uint64_t* masks, int64_t B, int32_t E, int32_t N, AdjSrc* s) {
+  if (!adj) return fail("adj is null");
+  if (B < 0) return fail("B < 0");
+  if (E <= 0 || E > 256) return fail("E must be in [1, 256]");
+  if (masks && (N <= 0 || B % N != 0)) return fail("compact layout: B must be a multiple of N > 0");
+  s->adj = adj;
+  s->masks = masks;
+  s->B = B;
+  s->E = E;
+  s->N = masks ? N : 1;
+  s->W = (E + 63) / 64;
+  s->inv_e = 1.0f / (float)E;
+  return 0;
+}
+
+size_t scan_temp_bytes(int64_t B) {
+  size_t bytes = 0;
+  hipcub::DeviceScan::InclusiveSum(nullptr, bytes, (const int64_t*)nullptr, (int64_t*)nullptr, (int)B);
+  return bytes;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* lsm_edges_last_error(void) { return g_err; }
+
+size_t lsm_edges_workspace_bytes(int64_t B) {
+  const size_t counts = ((size_t)B * sizeof(int64_t) + 255) & ~(size_t)255;
+  return counts + scan_temp_bytes(B) + 256;
+}
+
+int lsm_edges_count(const float* adj, const uint64_t* masks, int64_t B, int32_t E, int32_t N,
+                    int64_t* offsets, void* workspace, size_t workspace_bytes, void* stream) {
+  AdjSrc s;
+  if (make_src(adj, masks, B, E, N, &s)) return 1;
+  if (B > INT32_MAX) return fail("B exceeds the scan's int32 item count");
+  if (!offsets) return fail("offsets is null");
+  if (workspace_bytes < lsm_edges_workspace_bytes(B)) return fail("workspace too small");
+  hipStream_t st = (hipStream_t)stream;
+  zero_first<<<1, 1, 0, st>>>(offsets);
+  if (B == 0) return hipGetLastError() == hipSuccess ? 0 : fail("launch failed");
+  int64_t* counts = (int64_t*)workspace;
+  const size_t cbytes = ((size_t)B * sizeof(int64_t) + 255) & ~(size_t)255;
+  void* temp = (char*)workspace + cbytes;
+  size_t tbytes = workspace_bytes - cbytes;
+  const int64_t blocks = (B + GRAPHS_PER_BLOCK - 1) / GRAPHS_PER_BLOCK;
+  edge_count_kernel<<<dim3((unsigned)blocks), 256, 0, st>>>(s, counts);
+  if (hipcub::DeviceScan::InclusiveSum(temp, tbytes, counts, offsets + 1, (int)B, st) != hipSuccess)
+    return fail("scan failed");
+  return hipGetLastError() == hipSuccess ? 0 : fail("launch failed");
+}
+
+int lsm_edges_emit(const float* adj, const uint64_t* masks, int64_t B, int32_t E, int32_t N,
+                   const int64_t* offsets, int64_t nnz, int64_t* edge_index, float* edge_attr,
+                   void* stream) {
+  AdjSrc s;
+  if (make_src(adj, masks, B, E, N, &s)) return 1;
+  if (!offsets) return fail("offsets is null");
+  if (nnz < 0) return fail("nnz < 0");
+  if (nnz > 0 && (!edge_index || !edge_attr)) return fail("edge_index / edge_attr is null");
+  if (B == 0 || nnz == 0) return 0;
+  const int64_t blocks = (B + GRAPHS_PER_BLOCK - 1) / GRAPHS_PER_BLOCK;
+  edge_emit_kernel<<<dim3((unsigned)blocks), 256, 0, (hipStream_t)stream>>>(s, offsets, nnz, edge_index,
+                                                                           edge_attr);
+  return hipGetLastError() == hipSuccess ? 0 : fail("launch failed");
+}
+
+}  // extern "C"

@@ -10,30 +10,54 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(os.path.dirname(HERE), "csrc")
-SRC = os.path.join(CSRC, "lsm_rollout.hip")
+SRC = os.path.join(CSRC, "lsm_rollout.hip")   # the rollout TU (diagnostic builds recompile it alone)
 OUT = os.path.join(CSRC, "liblsm_rollout.so")
-DEPS = [SRC, os.path.join(CSRC, "lsm_numeric.h"), os.path.join(CSRC, "lsm_scenario.h"),
-        os.path.join(CSRC, "lsm_block.h"),
-        os.path.join(os.path.dirname(os.path.dirname(HERE)), "include", "lsm_rollout.h")]
+HDR = os.path.join(os.path.dirname(os.path.dirname(HERE)), "include", "lsm_rollout.h")
+# translation units -> their dependencies (each compiled to its own object, then linked)
+UNITS = {
+    "lsm_rollout.hip": ["lsm_numeric.h", "lsm_scenario.h", "lsm_block.h"],
+    "lsm_edges.hip": [],
+}
 
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC",
          # reproduce numpy's float64 expression order exactly; explicit fma() only where
          # OpenBLAS fuses (lsm_numeric.h)
          "-ffp-contract=off", "-Wno-unused-result"]
 
 
-def needs_build() -> bool:
-    if not os.path.exists(OUT):
+def _stale(target: str, deps) -> bool:
+    if not os.path.exists(target):
         return True
-    t = os.path.getmtime(OUT)
-    return any(os.path.getmtime(d) > t for d in DEPS if os.path.exists(d))
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
+
+
+def _obj(unit: str) -> str:
+    return os.path.join(CSRC, unit.rsplit(".", 1)[0] + ".o")
+
+
+def needs_build() -> bool:
+    objs = [_obj(u) for u in UNITS]
+    return _stale(OUT, objs) or any(
+        _stale(_obj(u), [os.path.join(CSRC, u), HDR] + [os.path.join(CSRC, d) for d in deps])
+        for u, deps in UNITS.items())
 
 
 def build(force: bool = False, verbose: bool = True) -> str:
     if not force and not needs_build():
         return OUT
-    cmd = [HIPCC] + FLAGS + ["-o", OUT + ".tmp", SRC]
+    objs = []
+    for u, deps in UNITS.items():
+        o = _obj(u)
+        objs.append(o)
+        if force or _stale(o, [os.path.join(CSRC, u), HDR] + [os.path.join(CSRC, d) for d in deps]):
+            cmd = [HIPCC] + FLAGS + ["-c", "-o", o + ".tmp", u]
+            if verbose:
+                print(" ".join(cmd), flush=True)
+            subprocess.check_call(cmd, cwd=CSRC)
+            os.replace(o + ".tmp", o)
+    cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", OUT + ".tmp"] + objs
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.check_call(cmd, cwd=CSRC)

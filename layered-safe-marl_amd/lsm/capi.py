@@ -28,7 +28,8 @@ INFO_FIELDS = ("individual_reward", "min_relative_distance", "Dist_to_goal", "Ti
 EXPORTED = ("lsm_create", "lsm_destroy", "lsm_last_error", "lsm_set_value_table", "lsm_set_ttr_table",
             "lsm_bind_output", "lsm_output_bytes", "lsm_reset", "lsm_step", "lsm_num_entities",
             "lsm_node_features", "lsm_obs_dim", "lsm_host_mt_uniforms", "lsm_host_scenario",
-            "lsm_set_agent_state")
+            "lsm_set_agent_state", "lsm_edges_workspace_bytes", "lsm_edges_count", "lsm_edges_emit",
+            "lsm_edges_last_error")
 
 
 class LsmConfig(C.Structure):
@@ -79,6 +80,10 @@ def load_library(path: str = LIB_PATH):
         "lsm_host_mt_uniforms": (I32, [U32, I32, D, D, P]),
         "lsm_host_scenario": (I32, [C.POINTER(LsmConfig), C.POINTER(LsmCurriculum), U32, P, P]),
         "lsm_set_agent_state": (I32, [P, I32, P, P, P]),
+        "lsm_edges_workspace_bytes": (SZ, [I64]),
+        "lsm_edges_count": (I32, [P, P, I64, I32, I32, P, P, SZ, P]),
+        "lsm_edges_emit": (I32, [P, P, I64, I32, I32, P, I64, P, P, P]),
+        "lsm_edges_last_error": (C.c_char_p, []),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

@@ -1,0 +1,81 @@
+"""Device-side ``GNNBase.process_adj`` (``onpolicy/algorithms/utils/gnn.py:376-407``).
+
+``process_adj(adj)`` takes the rollout's adjacency (a CUDA float32 tensor ``(B, E, E)`` or
+``(E, E)``, e.g. ``GpuGraphVecEnv.t_adj`` viewed as ``(n*N, E, E)``) and returns
+``(edge_index int64 [2, nnz], edge_attr float32 [nnz, 1])`` in ``nonzero()`` order, the pair the
+reference's GNN consumes. ``process_adj_compact(A, masks, N)`` does the same for the compact layout
+(``LSM_ADJ_COMPACT``: one ``[n, E, E]`` table + per-ego disconnect masks), expanding each ego's
+matrix on the fly instead of materialising ``(n, N, E, E)``.
+
+Like ``torch.nonzero`` the call synchronises once (the edge count sizes the outputs). All work runs
+in ``lsm_edges.hip`` through the C ABI; there is no torch/CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+from . import capi
+
+
+class EdgeError(RuntimeError):
+    pass
+
+
+def _torch():
+    import torch
+    return torch
+
+
+def _check(rc, lib):
+    if rc != 0:
+        raise EdgeError(lib.lsm_edges_last_error().decode())
+
+
+def _run(adj, masks, B, E, N):
+    torch = _torch()
+    lib = capi.load_library()
+    dev = adj.device
+    if dev.type != "cuda":
+        raise EdgeError("process_adj needs a CUDA (HIP) tensor; the edge list is built on the GPU")
+    stream = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    offsets = torch.empty(B + 1, dtype=torch.int64, device=dev)
+    ws_bytes = int(lib.lsm_edges_workspace_bytes(B))
+    ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
+    mp = C.c_void_p(masks.data_ptr()) if masks is not None else None
+    _check(lib.lsm_edges_count(C.c_void_p(adj.data_ptr()), mp, B, E, N, C.c_void_p(offsets.data_ptr()),
+                               C.c_void_p(ws.data_ptr()), ws_bytes, stream), lib)
+    nnz = int(offsets[B].item())   # the one sync, as in torch.nonzero
+    edge_index = torch.empty((2, nnz), dtype=torch.int64, device=dev)
+    edge_attr = torch.empty((nnz, 1), dtype=torch.float32, device=dev)
+    if nnz:
+        _check(lib.lsm_edges_emit(C.c_void_p(adj.data_ptr()), mp, B, E, N, C.c_void_p(offsets.data_ptr()),
+                                  nnz, C.c_void_p(edge_index.data_ptr()), C.c_void_p(edge_attr.data_ptr()),
+                                  stream), lib)
+    return edge_index, edge_attr
+
+
+def process_adj(adj):
+    """gnn.py:376-407 on a (B, E, E) or (E, E) float32 CUDA tensor."""
+    torch = _torch()
+    if not (2 <= adj.dim() <= 3) or adj.size(-1) != adj.size(-2):
+        raise EdgeError("adj must be (B, E, E) or (E, E)")   # the reference asserts the same
+    if adj.dtype != torch.float32:
+        raise EdgeError("adj must be float32 (the runner's buffer dtype, graph_buffer.py:95-104)")
+    a = adj.contiguous()
+    E = a.size(-1)
+    B = a.size(0) if a.dim() == 3 else 1
+    return _run(a, None, B, E, 1)
+
+
+def process_adj_compact(table, masks, num_agents: int):
+    """Edges of the per-ego graphs of a compact-layout adjacency: ``table`` [n, E, E] float32,
+    ``masks`` [n, N, ceil(E/64)] int64 (bit r of ego e = entity r disconnected). Graph b = env*N +
+    ego, so the result equals ``process_adj(expand_compact_adj(table, masks, E).view(-1, E, E))``."""
+    torch = _torch()
+    n, E = table.size(0), table.size(-1)
+    W = (E + 63) // 64
+    if table.dtype != torch.float32 or tuple(table.shape) != (n, E, E):
+        raise EdgeError("table must be float32 [n, E, E]")
+    if tuple(masks.shape) != (n, num_agents, W) or masks.dtype != torch.int64:
+        raise EdgeError("masks must be int64 [n, N, ceil(E/64)]")
+    return _run(table.contiguous(), masks.contiguous(), n * num_agents, E, num_agents)

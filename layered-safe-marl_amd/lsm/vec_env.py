@@ -84,7 +84,9 @@ def expand_compact_adj(adj, mask, E):
     sh = torch.arange(64, device=mask.device, dtype=torch.int64)
     bits = ((mask.unsqueeze(-1) >> sh) & 1).reshape(n, N, W * 64)[..., :E].bool()
     keep = ~(bits.unsqueeze(-1) | bits.unsqueeze(-2))
-    return adj.unsqueeze(1) * keep
+    # a select, not a product: masked entries are assigned 0 in the reference (in-place zeroing,
+    # navigation_graph_safe.py:976-989), whatever the table holds
+    return torch.where(keep, adj.unsqueeze(1), torch.zeros((), dtype=adj.dtype, device=adj.device))
 
 
 class GpuGraphVecEnv:
@@ -296,6 +298,15 @@ class GpuGraphVecEnv:
         if self.t_adj_mask is None:
             return self.t_adj
         return expand_compact_adj(self.t_adj, self.t_adj_mask, self.E)
+
+    def edge_list(self):
+        """The learner's graph input for the current per-ego adjacencies, as GNNBase.process_adj
+        (gnn.py:376-407) returns it for the runner's (n*N, E, E) batch: (edge_index int64 [2, nnz],
+        edge_attr float32 [nnz, 1]), built on the GPU from either adjacency layout."""
+        from . import edges
+        if self.t_adj_mask is None:
+            return edges.process_adj(self.t_adj.view(-1, self.E, self.E))
+        return edges.process_adj_compact(self.t_adj, self.t_adj_mask, self.N)
 
     def set_agent_state(self, env_index: int, agent_state, reached=None):
         """Overwrite one env's agent states ([N][4]) and optionally reached_goal ([N])."""

@@ -1,0 +1,182 @@
+"""GNNBase.process_adj (gnn.py:376-407) on the device: lsm_edges.hip through the C ABI vs the numpy
+oracle (oracle/process_adj.py), which is itself pinned here against torch.nonzero -- the call the
+reference makes -- on CPU tensors. Bit-exact: edge_index equal, edge_attr equal (a copy of the
+adjacency values, no arithmetic)."""
+import numpy as np
+import pytest
+
+from golden_replay import fixture_names, load
+from oracle.process_adj import expand_compact, process_adj as ora_process_adj
+
+
+def _torch_process_adj(adj):
+    """The reference's own expressions (gnn.py:392-406), run with torch on the CPU."""
+    import torch
+    adj = torch.as_tensor(adj)
+    if adj.dim() == 3:
+        E = adj.shape[1]
+        ei = adj.nonzero(as_tuple=False)
+        attr = adj[ei[:, 0], ei[:, 1], ei[:, 2]]
+        batch = ei[:, 0] * E
+        ei = torch.stack([batch + ei[:, 1], batch + ei[:, 2]], dim=0)
+    else:
+        ei = adj.nonzero(as_tuple=False).t().contiguous()
+        attr = adj[ei[0], ei[1]]
+    return ei.numpy(), attr.unsqueeze(1).numpy()
+
+
+def _random_adj(rng, B, E, density=0.3, specials=True):
+    a = rng.uniform(0.01, 2.0, (B, E, E)).astype(np.float32)
+    a[rng.random((B, E, E)) > density] = 0.0
+    if specials and B * E * E > 8:
+        flat = a.reshape(-1)
+        idx = rng.choice(flat.size, 4, replace=False)
+        flat[idx[0]] = -0.0            # not an edge (torch: -0.0 == 0)
+        flat[idx[1]] = np.nan          # an edge (NaN != 0)
+        flat[idx[2]] = -1.5            # negative values are edges too
+        flat[idx[3]] = np.float32(1e-38)
+    if B > 2:
+        a[1] = 0.0                     # an empty graph inside the batch
+    return a
+
+
+def _random_masks(rng, n, N, E):
+    W = (E + 63) // 64
+    m = rng.integers(0, 2 ** 63, (n, N, W), dtype=np.int64)
+    sparse = rng.random((n, N, W)) < 0.7   # mostly connected, like the common step
+    m[sparse] &= rng.integers(0, 2 ** 63, (int(sparse.sum()),), dtype=np.int64) & \
+        rng.integers(0, 2 ** 63, (int(sparse.sum()),), dtype=np.int64) & 0x0F0F0F0F0F0F0F0F
+    tail = E - 64 * (W - 1)
+    if tail < 64:
+        m[:, :, W - 1] &= (1 << tail) - 1
+    return m
+
+
+def _assert_same(got, want):
+    ge, ga = got
+    we, wa = want
+    assert ge.dtype == np.int64 and ge.shape == we.shape
+    np.testing.assert_array_equal(ge, we)
+    assert ga.shape == wa.shape and ga.dtype == np.float32
+    np.testing.assert_array_equal(ga, wa)   # NaN == NaN positions via assert_array_equal
+
+
+# ---------------- CPU: pin the oracle ----------------
+
+@pytest.mark.parametrize("B,E", [(1, 9), (5, 24), (3, 48), (2, 192), (4, 1)])
+def test_oracle_matches_torch_nonzero(B, E):
+    rng = np.random.default_rng(B * 1000 + E)
+    a = _random_adj(rng, B, E)
+    _assert_same(ora_process_adj(a), _torch_process_adj(a))
+    _assert_same(ora_process_adj(a[0]), _torch_process_adj(a[0]))
+
+
+def test_oracle_on_golden_adjacency():
+    for name in fixture_names():
+        z, meta = load(name)
+        for k in [k for k in z.files if k.endswith("_adj")][:3]:
+            adj = np.asarray(z[k], dtype=np.float32)
+            E = adj.shape[-1]
+            flat = adj.reshape(-1, E, E)
+            _assert_same(ora_process_adj(flat), _torch_process_adj(flat))
+
+
+def test_oracle_expand_compact_matches_host_expansion():
+    import torch
+    from lsm.vec_env import expand_compact_adj
+    rng = np.random.default_rng(5)
+    for (n, N, E) in [(3, 8, 24), (2, 64, 192), (2, 3, 9)]:
+        A = _random_adj(rng, n, E, specials=False)
+        M = _random_masks(rng, n, N, E)
+        want = expand_compact_adj(torch.as_tensor(A), torch.as_tensor(M), E).numpy()
+        np.testing.assert_array_equal(expand_compact(A, M), want)
+
+
+def test_wrapper_rejects_host_tensors_and_bad_shapes():
+    import torch
+    from lsm import edges
+    with pytest.raises(edges.EdgeError):
+        edges.process_adj(torch.zeros(2, 3, 4))
+    with pytest.raises(edges.EdgeError):
+        edges.process_adj(torch.zeros(2, 3, 3, dtype=torch.float64))
+    with pytest.raises(edges.EdgeError):
+        edges.process_adj(torch.zeros(2, 3, 3))   # CPU tensor: no fallback
+
+
+# ---------------- GPU: the HIP path ----------------
+
+def _gpu(x):
+    import torch
+    return torch.as_tensor(x).to("cuda:0")
+
+
+def _run_ref(a):
+    from lsm import edges
+    ei, ea = edges.process_adj(_gpu(a))
+    return ei.cpu().numpy(), ea.cpu().numpy()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,E", [(1, 1), (7, 9), (1000, 24), (257, 48), (33, 192), (3, 256), (5, 65)])
+def test_gpu_process_adj_reference_layout(B, E):
+    rng = np.random.default_rng(B + 7 * E)
+    a = _random_adj(rng, B, E)
+    _assert_same(_run_ref(a), ora_process_adj(a))
+
+
+@pytest.mark.gpu
+def test_gpu_process_adj_2d_empty_and_dense():
+    rng = np.random.default_rng(1)
+    a = _random_adj(rng, 1, 24)[0]
+    _assert_same(_run_ref(a), ora_process_adj(a))
+    z = np.zeros((4, 24, 24), np.float32)
+    ei, ea = _run_ref(z)
+    assert ei.shape == (2, 0) and ea.shape == (0, 1)
+    d = rng.uniform(0.5, 1.0, (6, 48, 48)).astype(np.float32)   # every entry an edge
+    _assert_same(_run_ref(d), ora_process_adj(d))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,N,E", [(3, 3, 9), (64, 8, 24), (9, 16, 48), (5, 64, 192)])
+def test_gpu_process_adj_compact_layout(n, N, E):
+    from lsm import edges
+    rng = np.random.default_rng(n * N)
+    A = _random_adj(rng, n, E)
+    M = _random_masks(rng, n, N, E)
+    ei, ea = edges.process_adj_compact(_gpu(A), _gpu(M), N)
+    want = ora_process_adj(expand_compact(A, M).reshape(-1, E, E))
+    _assert_same((ei.cpu().numpy(), ea.cpu().numpy()), want)
+
+
+@pytest.mark.gpu
+def test_gpu_process_adj_golden_adjacency():
+    for name in fixture_names():
+        z, meta = load(name)
+        for k in [k for k in z.files if k.endswith("_adj")]:
+            adj = np.asarray(z[k], dtype=np.float32)
+            E = adj.shape[-1]
+            flat = np.ascontiguousarray(adj.reshape(-1, E, E))
+            _assert_same(_run_ref(flat), ora_process_adj(flat))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("layout", ["reference", "compact"])
+def test_gpu_env_edge_list_full_size(layout):
+    """Config 3 size (8 agents x 4096 envs): the env's own edge list vs the oracle on its adjacency,
+    over a few steps with auto-resets; both layouts give the same edges."""
+    import torch
+    from lsm import hj_tables
+    from lsm.config import EnvArgs
+    from lsm.vec_env import GpuGraphVecEnv
+    args = EnvArgs(num_agents=8, num_env_steps=250 * 4, use_safety_filter=True, seed=0)
+    vt, _ = hj_tables.default_tables("double_integrator", small=True)
+    env = GpuGraphVecEnv(args, num_envs=4096, device="cuda:0", value_table=vt, return_numpy=False,
+                         build_infos=False, adj_layout=layout)
+    env.reset(4)
+    g = torch.Generator(device="cuda:0").manual_seed(3)
+    for t in range(3):
+        env.step(torch.randint(0, 25, (4096, 8), generator=g, device="cuda:0", dtype=torch.int32), 4)
+        ei, ea = env.edge_list()
+        ref = env.reference_adj().reshape(-1, env.E, env.E).cpu().numpy()
+        _assert_same((ei.cpu().numpy(), ea.cpu().numpy()), ora_process_adj(ref))
+    env.close()
