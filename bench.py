@@ -154,6 +154,9 @@ def main():
     ap.add_argument("--envs", type=int, default=0, help="envs per GPU (default: config's)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-cores", type=int, default=0)
+    ap.add_argument("--buffer", action="store_true",
+                    help="step through lsm.buffer.DeviceGraphBuffer: outputs written straight into "
+                         "GraphReplayBuffer-shaped rows + the insert kernel (runner hand-off included)")
     ap.add_argument("--edges", action="store_true",
                     help="also time GNNBase.process_adj (lsm_edges.hip) on the final adjacency and add an "
                          "'edges' object to the JSON line (SURVEY 8(f) row 2; not part of the step)")
@@ -192,12 +195,23 @@ def main():
     # timed region (the policy is outside the path; one env-step = one rollout_kernel launch).
     acts_all = torch.randint(0, 25, (a.warmup + a.steps, n_envs, N), generator=gen, device=dev,
                              dtype=torch.int32)
-    env.reset(ep)
     epl = c["episode_length"]
+    buf = None
+    if a.buffer:
+        from lsm.buffer import DeviceGraphBuffer
+        buf = DeviceGraphBuffer(env, episode_length=epl)
+        buf.warmup(ep)
+    else:
+        env.reset(ep)
 
     def one_step(t):
-        env.step_async(acts_all[t], ep)
-        env.step_wait()
+        if buf is not None:
+            buf.insert_step(acts_all[t], ep)
+            if buf.step == 0:
+                buf.after_update()
+        else:
+            env.step_async(acts_all[t], ep)
+            env.step_wait()
         if (t + 1) % epl == 0:   # episode boundary: RCCL reduction of the episode summary
             global_episode_summary(env.t_epinfo)
 
@@ -245,7 +259,9 @@ def main():
                                          "per-ego node_obs fp32; compact adjacency (E x E fp32 + per-ego "
                                          "u64 disconnect masks, lossless)"),
                        "hj_table": "synthetic %s" % (str(vt.shape) if vt is not None else "none"),
-                       "parallelism": "env-sharded dp%d" % world},
+                       "parallelism": "env-sharded dp%d" % world,
+                       "handoff": ("DeviceGraphBuffer rows (ring-bound outputs + insert kernel)" if a.buffer
+                                   else "env output tensors")},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
                          "frac": achieved / PEAK_HBM_GBPS, "traffic": traffic, "traffic_unit": "HBM bytes/launch (rocprofv3 PMC)",
                          "kernel": "%s<%d>" % ("rollout_block_kernel" if sb["block"] else "rollout_kernel",

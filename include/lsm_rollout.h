@@ -140,6 +140,17 @@ int lsm_step(lsm_env* env, const void* actions_device, int32_t action_kind,
 int lsm_set_agent_state(lsm_env* env, int32_t env_index, const double* agent_state,
                         const int32_t* reached, void* hip_stream);
 
+/* Ring-bound outputs: write slot `slot` of ring index i at base + (i + index_offset) * stride_bytes
+ * when 0 <= i + index_offset < count, else at the plain lsm_bind_output pointer. Binds the rows of
+ * a caller's [T][...] replay buffer (GraphReplayBuffer, onpolicy/utils/graph_buffer.py:84-163) so
+ * the step writes obs/node_obs/adj into buffer[t+1] and rewards into rewards[t] with no copy --
+ * what GMPERunner.insert's `.copy()`s do (graph_mpe_runner.py:444-487, graph_buffer.py:223-249).
+ * count <= 0 unbinds. lsm_select_ring(i) picks the index used by the following lsm_step /
+ * lsm_reset calls (host-side only: no upload, no sync); -1 = plain bindings. */
+int lsm_bind_output_ring(lsm_env* env, int32_t slot, void* base, size_t stride_bytes, int32_t count,
+                         int32_t index_offset);
+int lsm_select_ring(lsm_env* env, int32_t index);
+
 /* Shape helpers. */
 int32_t lsm_num_entities(const lsm_env* env);   /* E = N * (1 + L) */
 int32_t lsm_node_features(const lsm_env* env);  /* F */
@@ -169,6 +180,17 @@ int lsm_edges_emit(const float* adj, const uint64_t* masks, int64_t B, int32_t E
                    const int64_t* offsets, int64_t nnz, int64_t* edge_index, float* edge_attr,
                    void* hip_stream);
 const char* lsm_edges_last_error(void);
+
+/* ---- Buffer insert: the derived rows of GMPERunner.insert / warmup (lsm_buffer.hip) ----------
+ * Replaces graph_mpe_runner.py:444-487 (masks, active_masks, share_obs, share_agent_id) and the
+ * agent_id rows, for one buffer index, from obs [n][N][OBS] f32 and dones [n][N] u8 (NULL at
+ * warmup: masks untouched). centralized = args.use_centralized_V: share_obs [n][N][N*OBS] and
+ * share_agent_id [n][N][N], else [n][N][OBS] / [n][N][1]. masks / active_masks f32 [n][N][1],
+ * agent_id int32 [n][N][1]. */
+int lsm_buffer_insert(const float* obs, const uint8_t* dones, int32_t n, int32_t N, int32_t OBS,
+                      int32_t centralized, float* share_obs, int32_t* agent_id, int32_t* share_agent_id,
+                      float* masks, float* active_masks, void* hip_stream);
+const char* lsm_buffer_last_error(void);
 
 #ifdef __cplusplus
 }

@@ -29,6 +29,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <string>
 #include <vector>
 
@@ -2108,6 +2109,17 @@ struct lsm_env {
   int device;
   KParams* dparams;   // device copy of the per-handle constants (re-uploaded when dirty)
   bool params_dirty;
+  // ring-bound output slots (lsm_bind_output_ring): ring index i writes slot s at
+  // ring_base[s] + (i + ring_off[s]) * ring_stride[s] when that lands in [0, ring_count[s]),
+  // else at out_ptr[s]. One KParams copy per ring index lives in dring; selecting an index is a
+  // host-side pointer choice (no upload, no sync per step).
+  void* ring_base[LSM_NUM_OUT];
+  size_t ring_stride[LSM_NUM_OUT];
+  int32_t ring_count[LSM_NUM_OUT], ring_off[LSM_NUM_OUT];
+  int32_t ring_len;    // number of ring indices (0: no ring slots)
+  int32_t ring_cap;    // KParams copies allocated in dring
+  int32_t ring_sel;    // -1: plain bindings
+  KParams* dring;
   int lpe;   // lanes per env
   bool block;   // workgroup-per-env kernel (N > 32 or E > 64, or LSM_KERNEL=block)
   bool generic_only;   // LSM_GENERIC=1: never use the compile-time-N kernels (tests): 64 (one env per wave), 32 or 16 (2 or 4 envs per wave)
@@ -2245,6 +2257,10 @@ int lsm_create(const lsm_config* cfg, lsm_env** out) {
   e->cfg = *cfg;
   e->tables_ok = false;
   e->dparams = nullptr;
+  for (int k = 0; k < LSM_NUM_OUT; ++k) {
+    e->ring_base[k] = nullptr; e->ring_stride[k] = 0; e->ring_count[k] = 0; e->ring_off[k] = 0;
+  }
+  e->ring_len = 0; e->ring_cap = 0; e->ring_sel = -1; e->dring = nullptr;
   e->params_dirty = true;
   e->ttr_max = 0.0;
   memset(&e->val, 0, sizeof(e->val));
@@ -2449,6 +2465,40 @@ int lsm_bind_output(lsm_env* e, int32_t slot, void* ptr, size_t bytes) {
   return 0;
 }
 
+int lsm_bind_output_ring(lsm_env* e, int32_t slot, void* base, size_t stride_bytes, int32_t count,
+                         int32_t index_offset) {
+  if (!e) return 1;
+  if (slot < 0 || slot >= LSM_NUM_OUT) return fail(e, "bad output slot");
+  if (slot == LSM_OUT_RESET_FLAG || slot == LSM_OUT_EP_INFO || slot == LSM_OUT_EDGES ||
+      slot == LSM_OUT_DEBUG_STAMPS)
+    return fail(e, "slot " + std::to_string(slot) + " cannot be ring-bound");
+  if (count <= 0 || !base) {   // unbind
+    e->ring_count[slot] = 0;
+  } else {
+    if (stride_bytes < lsm_output_bytes(e, slot))
+      return fail(e, "ring stride smaller than slot " + std::to_string(slot) + "'s output");
+    e->ring_base[slot] = base;
+    e->ring_stride[slot] = stride_bytes;
+    e->ring_count[slot] = count;
+    e->ring_off[slot] = index_offset;
+  }
+  int len = 0;
+  for (int s = 0; s < LSM_NUM_OUT; ++s)
+    if (e->ring_count[s] > 0) len = std::max(len, e->ring_count[s] - e->ring_off[s]);
+  e->ring_len = len;
+  if (e->ring_sel >= len) e->ring_sel = -1;
+  e->params_dirty = true;
+  return 0;
+}
+
+int lsm_select_ring(lsm_env* e, int32_t index) {
+  if (!e) return 1;
+  if (index < -1 || index >= e->ring_len)
+    return fail(e, "ring index " + std::to_string(index) + " outside [-1, " + std::to_string(e->ring_len) + ")");
+  e->ring_sel = index;
+  return 0;
+}
+
 static int check_ready(lsm_env* e, bool stepping) {
   if (!e->tables_ok) return fail(e, "HJ value table (filter on) / TTR table (airtaxi) not set");
   const int req[] = {LSM_OUT_OBS, LSM_OUT_NODE_OBS, LSM_OUT_ADJ, LSM_OUT_REWARD, LSM_OUT_DONE,
@@ -2461,12 +2511,34 @@ static int check_ready(lsm_env* e, bool stepping) {
   return 0;
 }
 
+static const KParams* active_params(const lsm_env* e) {
+  return e->ring_sel >= 0 ? (const KParams*)(e->dring + e->ring_sel) : (const KParams*)e->dparams;
+}
+
+// output pointers of ring index i (see lsm_env::ring_*)
+static void apply_ring(const lsm_env* e, int i, KParams& P) {
+  auto at = [&](int slot, void* plain) -> void* {
+    if (e->ring_count[slot] <= 0) return plain;
+    const int j = i + e->ring_off[slot];
+    if (j < 0 || j >= e->ring_count[slot]) return plain;
+    return (char*)e->ring_base[slot] + (size_t)j * e->ring_stride[slot];
+  };
+  P.o.obs = (float*)at(LSM_OUT_OBS, P.o.obs);
+  P.o.node = (float*)at(LSM_OUT_NODE_OBS, P.o.node);
+  P.o.adj = (float*)at(LSM_OUT_ADJ, P.o.adj);
+  P.o.rew = (float*)at(LSM_OUT_REWARD, P.o.rew);
+  P.o.dones = (uint8_t*)at(LSM_OUT_DONE, P.o.dones);
+  P.o.info = (double*)at(LSM_OUT_INFO, P.o.info);
+  P.o.state = (double*)at(LSM_OUT_STATE, P.o.state);
+  P.o.adjmask = (uint64_t*)at(LSM_OUT_ADJ_MASK, P.o.adjmask);
+}
+
 extern "C++" template <int DYN, int LPE, int NT>
 static void launch_t(lsm_env* e, const KStep& L, size_t env_lds, hipStream_t st) {
   constexpr int G = WAVE / LPE;
   const int blocks = (e->cfg.num_envs + G - 1) / G;
   hipLaunchKernelGGL((rollout_kernel<DYN, LPE, NT>), dim3(blocks), dim3(WAVE), env_lds * G, st,
-                     (const KParams*)e->dparams, L);
+                     active_params(e), L);
 }
 
 extern "C++" template <int DYN, int NT>
@@ -2478,7 +2550,7 @@ static int launch_block_t(lsm_env* e, const KStep& L, size_t env_lds, hipStream_
     attr = true;
   }
   hipLaunchKernelGGL((rollout_block_kernel<DYN, NT>), dim3(e->cfg.num_envs), dim3(BT), env_lds, st,
-                     (const KParams*)e->dparams, L);
+                     active_params(e), L);
   return 0;
 }
 
@@ -2491,6 +2563,18 @@ static int launch(lsm_env* e, KStep& L, hipStream_t st) {
     fill_params(e, P);
     P.lds_env_bytes = (uint32_t)env_lds;
     HIPCHK(e, hipMemcpyAsync(e->dparams, &P, sizeof(P), hipMemcpyHostToDevice, st));
+    if (e->ring_len > 0) {
+      if (e->ring_cap < e->ring_len) {
+        if (dalloc(e, &e->dring, (size_t)e->ring_len)) return 1;
+        e->ring_cap = e->ring_len;
+      }
+      std::vector<KParams> ring((size_t)e->ring_len);
+      for (int i = 0; i < e->ring_len; ++i) {
+        ring[i] = P;
+        apply_ring(e, i, ring[i]);
+      }
+      HIPCHK(e, hipMemcpyAsync(e->dring, ring.data(), sizeof(KParams) * ring.size(), hipMemcpyHostToDevice, st));
+    }
     HIPCHK(e, hipStreamSynchronize(st));
     e->params_dirty = false;
   }

@@ -1,0 +1,115 @@
+"""Device-resident ``GraphReplayBuffer`` rows filled by the rollout with no copies.
+
+Mirrors the env-produced fields of ``onpolicy/utils/graph_buffer.py:84-163`` (share_obs, obs,
+node_obs, adj, agent_id, share_agent_id, rewards, masks, bad_masks, active_masks; same shapes and
+dtypes, as torch tensors on the env's GPU) and the env-side halves of ``GMPERunner.warmup``
+(``graph_mpe_runner.py:253-283``), ``GMPERunner.insert`` (``:444-487``) and
+``GraphReplayBuffer.after_update`` (``graph_buffer.py:253-283``).
+
+The rollout kernel writes obs / node_obs / adj into row t+1 and rewards into row t directly: the
+env's output slots are ring-bound to the buffer (``lsm_bind_output_ring``), one ring index per
+buffer row, so selecting a row is a host-side pointer choice. ``lsm_buffer_insert`` (HIP) then
+derives masks / active_masks / share_obs / share_agent_id / agent_id for that row from the step's
+obs and dones. Policy-side fields (rnn states, actions, values, log-probs) stay with the learner.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+from . import capi
+
+
+class BufferError(RuntimeError):
+    pass
+
+
+class DeviceGraphBuffer:
+    def __init__(self, env, episode_length=None, use_centralized_V: bool = True):
+        import torch
+        self.env = env
+        self.lib = capi.load_library()
+        self.T = int(episode_length or env.args.episode_length)
+        self.centralized = bool(use_centralized_V)
+        n, N, E, F, OBS = env.num_envs, env.N, env.E, env.F, env.OBS
+        dev = env.device
+        f32, i32 = torch.float32, torch.int32
+        T1 = self.T + 1
+        self.share_obs = torch.zeros((T1, n, N, N * OBS if self.centralized else OBS), dtype=f32, device=dev)
+        self.obs = torch.zeros((T1, n, N, OBS), dtype=f32, device=dev)
+        self.node_obs = torch.zeros((T1, n, N, E, F), dtype=f32, device=dev)
+        if env.t_adj_mask is None:
+            self.adj = torch.zeros((T1, n, N, E, E), dtype=f32, device=dev)
+            self.adj_mask = None
+        else:   # compact layout: one table per env + per-ego masks (expand with vec_env.expand_compact_adj)
+            self.adj = torch.zeros((T1, n, E, E), dtype=f32, device=dev)
+            self.adj_mask = torch.zeros((T1,) + tuple(env.t_adj_mask.shape), dtype=torch.int64, device=dev)
+        self.agent_id = torch.zeros((T1, n, N, 1), dtype=i32, device=dev)
+        self.share_agent_id = torch.zeros((T1, n, N, N if self.centralized else 1), dtype=i32, device=dev)
+        self.rewards = torch.zeros((self.T, n, N, 1), dtype=f32, device=dev)
+        self.masks = torch.ones((T1, n, N, 1), dtype=f32, device=dev)
+        self.bad_masks = torch.ones_like(self.masks)
+        self.active_masks = torch.ones_like(self.masks)
+        self.step = 0
+        self._bind()
+
+    # ring index i = buffer row i: obs-like rows at i, rewards at i - 1 (rewards[t] for step t)
+    def _bind(self):
+        rings = [(capi.OUT_OBS, self.obs, 0), (capi.OUT_NODE_OBS, self.node_obs, 0),
+                 (capi.OUT_ADJ, self.adj, 0), (capi.OUT_REWARD, self.rewards, -1)]
+        if self.adj_mask is not None:
+            rings.append((capi.OUT_ADJ_MASK, self.adj_mask, 0))
+        for slot, t, off in rings:
+            stride = t[0].numel() * t.element_size()
+            capi.check(self.lib.lsm_bind_output_ring(self.env.h, slot, C.c_void_p(t.data_ptr()), stride,
+                                                     t.shape[0], off), self.env.h)
+
+    def detach(self):
+        """Unbind the rings: the env writes its own output tensors again."""
+        for slot in (capi.OUT_OBS, capi.OUT_NODE_OBS, capi.OUT_ADJ, capi.OUT_REWARD, capi.OUT_ADJ_MASK):
+            capi.check(self.lib.lsm_bind_output_ring(self.env.h, slot, None, 0, 0, 0), self.env.h)
+        capi.check(self.lib.lsm_select_ring(self.env.h, -1), self.env.h)
+
+    def _select(self, i):
+        capi.check(self.lib.lsm_select_ring(self.env.h, int(i)), self.env.h)
+
+    def _insert(self, row, dones):
+        import torch
+        env = self.env
+        stream = C.c_void_p(torch.cuda.current_stream(env.device).cuda_stream)
+        dptr = C.c_void_p(dones.data_ptr()) if dones is not None else None
+        rc = self.lib.lsm_buffer_insert(
+            C.c_void_p(self.obs[row].data_ptr()), dptr, env.num_envs, env.N, env.OBS, int(self.centralized),
+            C.c_void_p(self.share_obs[row].data_ptr()), C.c_void_p(self.agent_id[row].data_ptr()),
+            C.c_void_p(self.share_agent_id[row].data_ptr()), C.c_void_p(self.masks[row].data_ptr()),
+            C.c_void_p(self.active_masks[row].data_ptr()), stream)
+        if rc != 0:
+            raise BufferError(self.lib.lsm_buffer_last_error().decode())
+
+    def warmup(self, num_current_episode: int = 0):
+        """GMPERunner.warmup (graph_mpe_runner.py:253-283): reset into row 0. Returns ep_info."""
+        self._select(0)
+        ep = self.env.reset(num_current_episode)[-1]
+        self._insert(0, None)
+        self.step = 0
+        return ep
+
+    def insert_step(self, actions, num_current_episode=None):
+        """env.step + GMPERunner.insert's env-side rows for buffer step t = self.step: obs,
+        node_obs, adj, share_obs, agent_id, share_agent_id, masks, active_masks at t+1 and
+        rewards at t. Returns (dones [n, N] u8, (info, reset_flag, ep_info)) device tensors."""
+        t = self.step
+        self._select(t + 1)
+        self.env.step_async(actions, num_current_episode)
+        self.env.step_wait()
+        self._insert(t + 1, self.env.t_done)
+        self.step = (t + 1) % self.T
+        return self.env.t_done, (self.env.t_info, self.env.t_reset, self.env.t_epinfo)
+
+    def after_update(self):
+        """GraphReplayBuffer.after_update (graph_buffer.py:253-283), env-side fields."""
+        fields = [self.share_obs, self.obs, self.node_obs, self.adj, self.agent_id, self.share_agent_id,
+                  self.masks, self.active_masks, self.bad_masks]
+        if self.adj_mask is not None:
+            fields.append(self.adj_mask)
+        for f in fields:
+            f[0].copy_(f[-1])

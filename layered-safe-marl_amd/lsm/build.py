@@ -17,6 +17,7 @@ HDR = os.path.join(os.path.dirname(os.path.dirname(HERE)), "include", "lsm_rollo
 UNITS = {
     "lsm_rollout.hip": ["lsm_numeric.h", "lsm_scenario.h", "lsm_block.h"],
     "lsm_edges.hip": [],
+    "lsm_buffer.hip": [],
 }
 
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

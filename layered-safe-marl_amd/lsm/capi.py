@@ -29,7 +29,8 @@ EXPORTED = ("lsm_create", "lsm_destroy", "lsm_last_error", "lsm_set_value_table"
             "lsm_bind_output", "lsm_output_bytes", "lsm_reset", "lsm_step", "lsm_num_entities",
             "lsm_node_features", "lsm_obs_dim", "lsm_host_mt_uniforms", "lsm_host_scenario",
             "lsm_set_agent_state", "lsm_edges_workspace_bytes", "lsm_edges_count", "lsm_edges_emit",
-            "lsm_edges_last_error")
+            "lsm_edges_last_error", "lsm_bind_output_ring", "lsm_select_ring", "lsm_buffer_insert",
+            "lsm_buffer_last_error")
 
 
 class LsmConfig(C.Structure):
@@ -84,6 +85,10 @@ def load_library(path: str = LIB_PATH):
         "lsm_edges_count": (I32, [P, P, I64, I32, I32, P, P, SZ, P]),
         "lsm_edges_emit": (I32, [P, P, I64, I32, I32, P, I64, P, P, P]),
         "lsm_edges_last_error": (C.c_char_p, []),
+        "lsm_bind_output_ring": (I32, [P, I32, P, SZ, I32, I32]),
+        "lsm_select_ring": (I32, [P, I32]),
+        "lsm_buffer_insert": (I32, [P, P, I32, I32, I32, I32, P, P, P, P, P, P]),
+        "lsm_buffer_last_error": (C.c_char_p, []),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

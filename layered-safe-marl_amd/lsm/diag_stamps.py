@@ -23,7 +23,8 @@ PHASES = ["load", "decode", "filter-pairs", "filter-ego", "integrate", "dist+min
 def build_stamps():
     from . import build
     cmd = [build.HIPCC] + build.FLAGS + ["-shared", "-DLSM_STAMPS", "-o", STAMP_LIB, build.SRC,
-                                        os.path.join(CSRC, "lsm_edges.hip")]
+                                        os.path.join(CSRC, "lsm_edges.hip"),
+                                        os.path.join(CSRC, "lsm_buffer.hip")]
     subprocess.check_call(cmd, cwd=CSRC)
 
 
