@@ -166,17 +166,109 @@ def ttr_table_from_stored(stored: dict) -> HjTable:
                    ttr_max=float(stored["ttr_max"]))
 
 
-def load_stored_pickle(path: str) -> dict:
-    """Read a value/TTR pickle written by this repo's own tools (never a third-party file)."""
+# ---- pickle ingestion that executes nothing from the file ----------------------------------
+# The reference's value/TTR pickles hold hj_reachability / hj_reachability_utils objects
+# (HjDataHandle, safety_filter.py:154-168; navigation_graph_safe.py:128-138) whose classes are absent
+# here. The unpickler below resolves only numpy's array/dtype reconstructors, codecs.encode and inert
+# builtin containers; every other global (a class or ANY callable, e.g. os.system) becomes an inert
+# stand-in that merely records its arguments and state. Arrays are then found by attribute name.
+
+_NP_OK = {"_reconstruct", "ndarray", "dtype", "scalar", "_frombuffer"}
+_BUILTIN_OK = {"dict", "list", "tuple", "set", "frozenset", "slice", "complex", "float", "int",
+               "bytearray", "bytes", "str", "bool", "range"}
+
+
+class _Inert:
+    """Stand-in for any global the safe unpickler will not resolve: calling it (REDUCE) or
+    constructing it (NEWOBJ) only stores the arguments; BUILD stores the state."""
+
+    def __init__(self, *args, **kwargs):
+        self._args, self._kwargs = args, kwargs
+
+    def __setstate__(self, state):
+        if isinstance(state, tuple) and len(state) == 2 and isinstance(state[1], dict):
+            state = {**(state[0] or {}), **state[1]}   # (dict, slotstate)
+        if isinstance(state, dict):
+            self.__dict__.update(state)
+        else:
+            self._state = state
+
+    def __getattr__(self, name):   # missing attributes of a stand-in are absent, never computed
+        raise AttributeError(name)
+
+
+class _SafeUnpickler(pickle.Unpickler):
+    def find_class(self, module, name):
+        top = module.split(".")[0]
+        if top == "numpy" and name in _NP_OK:
+            return super().find_class(module, name)
+        if module == "_codecs" and name == "encode":
+            return super().find_class(module, name)
+        if module == "builtins" and name in _BUILTIN_OK:
+            return super().find_class(module, name)
+        return type(name, (_Inert,), {"__module__": "lsm.hj_tables.inert." + module})
+
+
+def _find_array(x, depth=0):
+    """First ndarray inside x (an array, an array-like stand-in such as a pickled jax Array, or a
+    container of them)."""
+    if isinstance(x, np.ndarray):
+        return x
+    if depth > 6:
+        return None
+    if isinstance(x, (list, tuple)):
+        items = x
+    elif isinstance(x, dict):
+        items = list(x.values())
+    elif isinstance(x, _Inert):
+        items = list(getattr(x, "_args", ())) + list(x.__dict__.values())
+        if "_state" in x.__dict__:
+            items.append(x.__dict__["_state"])
+    else:
+        return None
+    for it in items:
+        a = _find_array(it, depth + 1)
+        if a is not None:
+            return a
+    return None
+
+
+def _get(obj, name, default=None):
+    if isinstance(obj, dict):
+        return obj.get(name, default)
+    return obj.__dict__.get(name, default) if hasattr(obj, "__dict__") else getattr(obj, name, default)
+
+
+def safe_load_pickle(path: str):
+    """Unpickle ``path`` without executing anything it names (see _SafeUnpickler)."""
     with open(path, "rb") as f:
-        obj = pickle.load(f)
-    meta = obj.grid_meta_data
-    d = dict(values=np.asarray(obj.values, dtype=F32), lo=np.asarray(meta.lo), hi=np.asarray(meta.hi),
-             shape=tuple(meta.shape), periodic=tuple(getattr(meta, "periodic_dims", ())))
-    if hasattr(obj, "info"):
-        d["separation_distance"] = float(obj.info["separation_distance"])
-    if hasattr(obj, "ttr_max"):
-        d["ttr_max"] = float(obj.ttr_max)
+        return _SafeUnpickler(f).load()
+
+
+def load_stored_pickle(path: str) -> dict:
+    """Read a value / TTR pickle (``.values``, ``.grid_meta_data`` {lo, hi, shape, periodic_dims},
+    ``.info['separation_distance']``, ``.ttr_max``) through the non-executing unpickler."""
+    obj = safe_load_pickle(path)
+    meta = _get(obj, "grid_meta_data")
+    if meta is None:
+        raise ValueError("%s: no grid_meta_data" % path)
+    vals = _find_array(_get(obj, "values"))
+    if vals is None:
+        raise ValueError("%s: no values array" % path)
+    lo, hi = _find_array(_get(meta, "lo")), _find_array(_get(meta, "hi"))
+    lo = np.asarray(lo if lo is not None else _get(meta, "lo"), dtype=np.float64)
+    hi = np.asarray(hi if hi is not None else _get(meta, "hi"), dtype=np.float64)
+    shape = _get(meta, "shape")
+    shape = tuple(int(v) for v in (shape if shape is not None else vals.shape))
+    per = _get(meta, "periodic_dims", ()) or ()
+    per = _find_array(per) if not isinstance(per, (list, tuple)) else per
+    d = dict(values=np.asarray(vals, dtype=F32), lo=lo, hi=hi, shape=shape,
+             periodic=tuple(int(v) for v in np.asarray(per).reshape(-1)) if per is not None else ())
+    info = _get(obj, "info")
+    if info is not None and _get(info, "separation_distance") is not None:
+        d["separation_distance"] = float(_get(info, "separation_distance"))
+    if _get(obj, "ttr_max") is not None:
+        d["ttr_max"] = float(_get(obj, "ttr_max"))
     return d
 
 
