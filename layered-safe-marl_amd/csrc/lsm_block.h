@@ -118,7 +118,7 @@ __device__ __forceinline__ void emit_graph_block(const KParams& P, Lds& S, int e
       for (int t = tid; t < EE / 4; t += BT) {
         const int u = 4 * t;
         const int r = qdiv<NT>(u, E, P.m_E), c = u - r * E;
-        st_stream(a + u, make_float4(adj_value(P, S, r, c), adj_value(P, S, r, c + 1), adj_value(P, S, r, c + 2),
+        st_stream<true>(a + u, make_float4(adj_value(P, S, r, c), adj_value(P, S, r, c + 1), adj_value(P, S, r, c + 2),
                                      adj_value(P, S, r, c + 3)));
       }
     } else {
@@ -148,7 +148,7 @@ __device__ __forceinline__ void emit_graph_block(const KParams& P, Lds& S, int e
           if (bits & 2u) w.y = 0.f;
           if (bits & 4u) w.z = 0.f;
           if (bits & 8u) w.w = 0.f;
-          st_stream(adj_out + (size_t)e * EE + u, w);
+          st_stream<true>(adj_out + (size_t)e * EE + u, w);
         }
       }
     } else {

@@ -254,9 +254,14 @@ __device__ __forceinline__ GAS T* gptr(T* p) {
 
 // One float4 of the per-step graph outputs. (Non-temporal stores were measured slower with
 // the filter on: 37.9 vs 35.9 us per step at config 3.)
+// Output stores. NTS = nontemporal (`nt`): measured on MI355X (profiles/r01_v9_nt_stores.txt)
+// +5 % at config 4 (airtaxi N = 16) and +8.5 % at config 5 (workgroup kernel), within noise
+// (-1 %) at config 3, so the N >= 16 one-wave kernels and the workgroup kernel use it.
+template <bool NTS = false>
 __device__ __forceinline__ void st_stream(GAS float* dst, float4 v) {
   const f32x4 x = {v.x, v.y, v.z, v.w};
-  *(GAS f32x4*)dst = x;
+  if (NTS) __builtin_nontemporal_store(x, (GAS f32x4*)dst);
+  else *(GAS f32x4*)dst = x;
 }
 
 // all() over the LPE-lane group of the calling lane (one env)
@@ -1180,7 +1185,7 @@ __device__ __forceinline__ void emit_adj_uniform(const KParams& P, const Lds& S,
       GAS float* dst = adj_out + (size_t)e * EE;
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        if (t0 + j * LPE <= last) st_stream(dst + u[j], w[j]);
+        if (t0 + j * LPE <= last) st_stream<(NT >= 16)>(dst + u[j], w[j]);
     }
   }
 }
@@ -1207,7 +1212,7 @@ __device__ __forceinline__ void emit_graph(const KParams& P, Lds& S, int env, bo
     // LSM_ADJ_COMPACT: the unmasked table once + the per-ego masks (one word: E <= 64)
     GAS float* a = gptr(P.o.adj) + (size_t)env * EE;
     if ((E & 3) == 0) {
-      for (int q = lane; q < EE / 4; q += LPE) st_stream(a + 4 * q, *(const float4*)(S.fval + 4 * q));
+      for (int q = lane; q < EE / 4; q += LPE) st_stream<(NT >= 16)>(a + 4 * q, *(const float4*)(S.fval + 4 * q));
     } else {
       for (int q = lane; q < EE; q += LPE) a[q] = S.fval[q];
     }
@@ -1242,7 +1247,7 @@ __device__ __forceinline__ void emit_graph(const KParams& P, Lds& S, int env, bo
           if (bits & 2u) w.y = 0.f;
           if (bits & 4u) w.z = 0.f;
           if (bits & 8u) w.w = 0.f;
-          st_stream(dst + u[j], w);
+          st_stream<(NT >= 16)>(dst + u[j], w);
         }
       }
     }
@@ -1286,7 +1291,7 @@ __device__ __forceinline__ void emit_nodes(const KParams& P, Lds& S, int env, bo
 #endif
       for (int e = 0; e < N; ++e) {
         const double* o = S.egooff + e * F;
-        st_stream(node_out + (size_t)e * E * F + 4 * t,
+        st_stream<(NT >= 16)>(node_out + (size_t)e * E * F + 4 * t,
             make_float4((float)(fv[0] - o[qq[0]]), (float)(fv[1] - o[qq[1]]), (float)(fv[2] - o[qq[2]]),
                         (float)(fv[3] - o[qq[3]])));
       }
