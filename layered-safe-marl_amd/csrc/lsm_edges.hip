@@ -19,9 +19,11 @@
 //   edge_emit_kernel    one wave per graph: re-reads its E*E values (L2 / MALL resident after the
 //                       count pass) and writes its edges at offsets[b] in row-major order; the
 //                       in-chunk position is the popcount of the ballot below the lane (mbcnt), so
-//                       the output order is exactly nonzero()'s.
-// A graph's E*E values are walked as one flat index k = r*E + c in 64-element chunks, so every
-// lane is busy whatever E is (E = 24 rows would leave 40 of 64 lanes idle per row).
+//                       the output order is exactly nonzero()'s; edges are compacted in LDS and
+//                       stored by consecutive lanes.
+// A graph's E*E values are walked as one flat index k = r*E + c in 64-lane chunks (4 elements per
+// lane with one 16-B load when E is even), so every lane is busy whatever E is (E = 24 rows would
+// leave 40 of 64 lanes idle per row).
 #include <hip/hip_runtime.h>
 #include <hipcub/device/device_scan.hpp>
 
@@ -30,6 +32,7 @@
 namespace {
 
 constexpr int WAVE = 64;
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 constexpr int GRAPHS_PER_BLOCK = 4;   // 256-thread workgroups, one wave per graph
 
 struct AdjSrc {
@@ -65,52 +68,125 @@ __device__ __forceinline__ const float* graph_ptr(const AdjSrc& s, int64_t b) {
   return s.adj + (s.masks ? (b / s.N) : b) * EE;
 }
 
-__global__ __launch_bounds__(256) void edge_count_kernel(AdjSrc s, int64_t* __restrict__ counts) {
+// VEC = 4 (E even, so every graph and row pair is 16-B aligned): each lane takes 4 consecutive
+// elements with one 16-B load; its nonzero count c in [0, 4] is spread over 3 ballots (bit k of c),
+// so the exclusive prefix over lanes is sum_k 2^k * popcount(ballot_k below the lane).
+template <int VEC>
+__device__ __forceinline__ int lane_vals(const AdjSrc& s, int64_t b, const float* g, const uint64_t* m, int k,
+                                         int EE, float (&v)[VEC]) {
+  int c = 0;
+  if (VEC == 1) {
+    v[0] = k < EE ? load_val(s, b, g, m, k) : 0.0f;
+    c = v[0] != 0.0f;
+  } else {
+    if (k < EE) {
+      const f32x4 q = __builtin_nontemporal_load((const f32x4*)(g + k));
+      v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+      if (m) {
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) {
+          const int r = row_of(k + i, s.inv_e);
+          if (masked(m, r, k + i - r * s.E)) v[i] = 0.0f;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) v[i] = 0.0f;
+    }
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) c += v[i] != 0.0f;   // NaN counts, -0.0 does not (torch)
+  }
+  return c;
+}
+
+__device__ __forceinline__ uint32_t below(uint64_t bal) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+}
+
+template <int VEC>
+__global__ __launch_bounds__(256) void edge_count_kernel(AdjSrc s, int64_t* __restrict__ counts,
+                                                         int64_t* __restrict__ offsets) {
   const int64_t b = (int64_t)blockIdx.x * GRAPHS_PER_BLOCK + (threadIdx.x >> 6);
   if (b >= s.B) return;   // whole wave exits together
   const float* g = graph_ptr(s, b);
   const uint64_t* m = s.masks ? s.masks + b * s.W : nullptr;
   const int EE = s.E * s.E;
   int cnt = 0;
-  for (int k0 = 0; k0 < EE; k0 += WAVE) {
-    const int k = k0 + lane_id();
-    const bool nz = k < EE && load_val(s, b, g, m, k) != 0.0f;   // NaN counts, -0.0 does not (torch)
-    cnt += __popcll(__ballot(nz));
+  for (int k0 = 0; k0 < EE; k0 += WAVE * VEC) {
+    float v[VEC];
+    const int c = lane_vals<VEC>(s, b, g, m, k0 + VEC * lane_id(), EE, v);
+    if (VEC == 1) {
+      cnt += __popcll(__ballot(c != 0));
+    } else {
+      cnt += __popcll(__ballot(c & 1)) + 2 * __popcll(__ballot(c & 2)) + 4 * __popcll(__ballot(c & 4));
+    }
   }
   if (lane_id() == 0) counts[b] = cnt;
+  if (b == 0 && lane_id() == 0) offsets[0] = 0;   // the scan fills offsets[1..B]
 }
 
+// The chunk's edges are first compacted into the wave's LDS slice (flat index + value at their
+// exclusive-prefix slot), then written out by consecutive lanes: every store instruction covers
+// consecutive edge slots (full 512-B / 256-B lines), where storing straight from the lane that found
+// the edge would scatter each instruction over partial lines.
+template <int VEC>
 __global__ __launch_bounds__(256) void edge_emit_kernel(AdjSrc s, const int64_t* __restrict__ offsets,
                                                         int64_t nnz, int64_t* __restrict__ edge_index,
                                                         float* __restrict__ edge_attr) {
-  const int64_t b = (int64_t)blockIdx.x * GRAPHS_PER_BLOCK + (threadIdx.x >> 6);
+  __shared__ int32_t sk[GRAPHS_PER_BLOCK][WAVE * VEC];
+  __shared__ float sv[GRAPHS_PER_BLOCK][WAVE * VEC];
+  const int w = threadIdx.x >> 6;
+  const int64_t b = (int64_t)blockIdx.x * GRAPHS_PER_BLOCK + w;
   if (b >= s.B) return;
   const float* g = graph_ptr(s, b);
   const uint64_t* m = s.masks ? s.masks + b * s.W : nullptr;
   const int EE = s.E * s.E;
+  const int lane = lane_id();
   const int64_t node0 = b * s.E;
   int64_t pos = offsets[b];
   const int64_t end = offsets[b + 1];
   if (end > nnz) return;   // caller's nnz is stale: write nothing rather than out of bounds
-  for (int k0 = 0; k0 < EE && pos < end; k0 += WAVE) {
-    const int k = k0 + lane_id();
-    const float v = k < EE ? load_val(s, b, g, m, k) : 0.0f;
-    const bool nz = v != 0.0f;
-    const uint64_t bal = __ballot(nz);
-    if (nz) {
-      const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
-                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-      const int64_t o = pos + below;
-      const int r = row_of(k, s.inv_e);
-      edge_index[o] = node0 + r;
-      edge_index[nnz + o] = node0 + (k - r * s.E);
-      edge_attr[o] = v;
+  for (int k0 = 0; k0 < EE && pos < end; k0 += WAVE * VEC) {
+    const int k = k0 + VEC * lane;
+    float v[VEC];
+    const int c = lane_vals<VEC>(s, b, g, m, k, EE, v);
+    uint32_t pre;
+    int tot;
+    if (VEC == 1) {
+      const uint64_t bal = __ballot(c != 0);
+      pre = below(bal);
+      tot = __popcll(bal);
+    } else {
+      const uint64_t b0 = __ballot(c & 1), b1 = __ballot(c & 2), b2 = __ballot(c & 4);
+      pre = below(b0) + 2 * below(b1) + 4 * below(b2);
+      tot = __popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2);
     }
-    pos += __popcll(bal);
+    if (c) {
+      int o = (int)pre;
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) {
+        if (v[i] != 0.0f) {
+          sk[w][o] = k + i;
+          sv[w][o] = v[i];
+          ++o;
+        }
+      }
+    }
+    // intra-wave LDS hand-off (the block's waves run different graphs: no block barrier)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (int t = lane; t < tot; t += WAVE) {
+      const int kk = sk[w][t];
+      const int r = row_of(kk, s.inv_e);
+      edge_index[pos + t] = node0 + r;
+      edge_index[nnz + pos + t] = node0 + (kk - r * s.E);
+      edge_attr[pos + t] = sv[w][t];
+    }
+    __builtin_amdgcn_wave_barrier();   // slots are rewritten by the next chunk
+    pos += tot;
   }
 }
-
-__global__ void zero_first(int64_t* offsets) { offsets[0] = 0; }
 
 thread_local char g_err[256];
 
@@ -159,14 +235,14 @@ int lsm_edges_count(const float* adj, const uint64_t* masks, int64_t B, int32_t 
   if (!offsets) return fail("offsets is null");
   if (workspace_bytes < lsm_edges_workspace_bytes(B)) return fail("workspace too small");
   hipStream_t st = (hipStream_t)stream;
-  zero_first<<<1, 1, 0, st>>>(offsets);
-  if (B == 0) return hipGetLastError() == hipSuccess ? 0 : fail("launch failed");
+  if (B == 0) return hipMemsetAsync(offsets, 0, sizeof(int64_t), st) == hipSuccess ? 0 : fail("memset failed");
   int64_t* counts = (int64_t*)workspace;
   const size_t cbytes = ((size_t)B * sizeof(int64_t) + 255) & ~(size_t)255;
   void* temp = (char*)workspace + cbytes;
   size_t tbytes = workspace_bytes - cbytes;
   const int64_t blocks = (B + GRAPHS_PER_BLOCK - 1) / GRAPHS_PER_BLOCK;
-  edge_count_kernel<<<dim3((unsigned)blocks), 256, 0, st>>>(s, counts);
+  if (E % 2 == 0) edge_count_kernel<4><<<dim3((unsigned)blocks), 256, 0, st>>>(s, counts, offsets);
+  else edge_count_kernel<1><<<dim3((unsigned)blocks), 256, 0, st>>>(s, counts, offsets);
   if (hipcub::DeviceScan::InclusiveSum(temp, tbytes, counts, offsets + 1, (int)B, st) != hipSuccess)
     return fail("scan failed");
   return hipGetLastError() == hipSuccess ? 0 : fail("launch failed");
@@ -182,8 +258,12 @@ int lsm_edges_emit(const float* adj, const uint64_t* masks, int64_t B, int32_t E
   if (nnz > 0 && (!edge_index || !edge_attr)) return fail("edge_index / edge_attr is null");
   if (B == 0 || nnz == 0) return 0;
   const int64_t blocks = (B + GRAPHS_PER_BLOCK - 1) / GRAPHS_PER_BLOCK;
-  edge_emit_kernel<<<dim3((unsigned)blocks), 256, 0, (hipStream_t)stream>>>(s, offsets, nnz, edge_index,
-                                                                           edge_attr);
+  if (E % 2 == 0)
+    edge_emit_kernel<4><<<dim3((unsigned)blocks), 256, 0, (hipStream_t)stream>>>(s, offsets, nnz, edge_index,
+                                                                                 edge_attr);
+  else
+    edge_emit_kernel<1><<<dim3((unsigned)blocks), 256, 0, (hipStream_t)stream>>>(s, offsets, nnz, edge_index,
+                                                                                 edge_attr);
   return hipGetLastError() == hipSuccess ? 0 : fail("launch failed");
 }
 
