@@ -51,6 +51,12 @@ class DeviceGraphBuffer:
         self.active_masks = torch.ones_like(self.masks)
         self.step = 0
         self._bind()
+        # per-row kernel arguments, built once (the per-step host path is two ctypes calls)
+        self._rows = [tuple(C.c_void_p(t[r].data_ptr()) for t in (self.obs, self.share_obs, self.agent_id,
+                                                                  self.share_agent_id, self.masks,
+                                                                  self.active_masks))
+                      for r in range(T1)]
+        self._done_ptr = C.c_void_p(env.t_done.data_ptr())
 
     # ring index i = buffer row i: obs-like rows at i, rewards at i - 1 (rewards[t] for step t)
     def _bind(self):
@@ -72,16 +78,11 @@ class DeviceGraphBuffer:
     def _select(self, i):
         capi.check(self.lib.lsm_select_ring(self.env.h, int(i)), self.env.h)
 
-    def _insert(self, row, dones):
-        import torch
+    def _insert(self, row, with_dones):
         env = self.env
-        stream = C.c_void_p(torch.cuda.current_stream(env.device).cuda_stream)
-        dptr = C.c_void_p(dones.data_ptr()) if dones is not None else None
-        rc = self.lib.lsm_buffer_insert(
-            C.c_void_p(self.obs[row].data_ptr()), dptr, env.num_envs, env.N, env.OBS, int(self.centralized),
-            C.c_void_p(self.share_obs[row].data_ptr()), C.c_void_p(self.agent_id[row].data_ptr()),
-            C.c_void_p(self.share_agent_id[row].data_ptr()), C.c_void_p(self.masks[row].data_ptr()),
-            C.c_void_p(self.active_masks[row].data_ptr()), stream)
+        o, so, aid, said, m, am = self._rows[row]
+        rc = self.lib.lsm_buffer_insert(o, self._done_ptr if with_dones else None, env.num_envs, env.N, env.OBS,
+                                        int(self.centralized), so, aid, said, m, am, env._stream())
         if rc != 0:
             raise BufferError(self.lib.lsm_buffer_last_error().decode())
 
@@ -89,7 +90,7 @@ class DeviceGraphBuffer:
         """GMPERunner.warmup (graph_mpe_runner.py:253-283): reset into row 0. Returns ep_info."""
         self._select(0)
         ep = self.env.reset(num_current_episode)[-1]
-        self._insert(0, None)
+        self._insert(0, False)
         self.step = 0
         return ep
 
@@ -101,7 +102,7 @@ class DeviceGraphBuffer:
         self._select(t + 1)
         self.env.step_async(actions, num_current_episode)
         self.env.step_wait()
-        self._insert(t + 1, self.env.t_done)
+        self._insert(t + 1, True)
         self.step = (t + 1) % self.T
         return self.env.t_done, (self.env.t_info, self.env.t_reset, self.env.t_epinfo)
 

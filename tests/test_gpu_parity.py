@@ -309,3 +309,53 @@ def test_gpu_config5_full_size_compact():
             np.testing.assert_allclose(obs[k].cpu().numpy(), r[0][0], rtol=0, atol=F32_ATOL)
             np.testing.assert_allclose(st[k].cpu().numpy(), o.envs[0].s, rtol=0, atol=STATE_ATOL)
     env.close()
+
+
+@pytest.mark.gpu
+def test_gpu_action_encodings_and_dummy_semantics():
+    """The runner's one-hot actions (float32 / float64, graph_mpe_runner.py:432-433) decode like
+    indices (environment.py:386-410); auto_reset=False (GraphDummyVecEnv, env_wrappers.py:918-928)
+    returns the 8-tuple, keeps stepping past the episode end without resetting, and matches the
+    oracle with auto_reset=False."""
+    import torch
+    c = dict(CASES[2])
+    ep = c.pop("ep")
+    c["episode_length"], c["num_env_steps"] = 12, 48
+    meta = dict(num_landmarks=2, n_rollout_threads=1, use_masking=True, num_internal_step=1, seed=2, ep=ep, **c)
+    n, N, T = 6, meta["num_agents"], 16
+    rng = np.random.default_rng(4)
+    acts = rng.integers(0, 25, (T, n, N))
+    envs = {k: _gpu_env(meta, n_envs=n, seed=2, return_numpy=True) for k in ("idx", "f32", "f64")}
+    for e in envs.values():
+        e.reset(meta["ep"])
+    eye = np.eye(25)
+    for t in range(T):
+        outs = {}
+        for k, e in envs.items():
+            a = acts[t] if k == "idx" else eye[acts[t]].astype(np.float32 if k == "f32" else np.float64)
+            if k == "f64":
+                a = torch.as_tensor(a, device="cuda:0")   # device one-hot tensor
+            outs[k] = e.step(a, meta["ep"])
+        for k in ("f32", "f64"):
+            for i in (0, 2, 3, 4, 5):
+                np.testing.assert_array_equal(outs[k][i], outs["idx"][i], err_msg="%s t=%d out %d" % (k, t, i))
+    for e in envs.values():
+        e.close()
+
+    gpu = _gpu_env(meta, n_envs=n, seed=2, return_numpy=True, auto_reset=False)
+    ora = _oracle_for(meta, 2, n)
+    ora.auto_reset = False
+    g, o = gpu.reset(meta["ep"]), ora.reset(meta["ep"])
+    np.testing.assert_allclose(g[0], o[0], rtol=0, atol=F32_ATOL)
+    for t in range(T):
+        g = gpu.step(acts[t], meta["ep"])
+        o = ora.step(acts[t], meta["ep"])
+        assert len(g) == 8 and g[7] == 0
+        np.testing.assert_array_equal(g[5], o[5], err_msg="t=%d" % t)
+        np.testing.assert_allclose(g[0], o[0], rtol=0, atol=F32_ATOL, err_msg="t=%d" % t)
+        np.testing.assert_allclose(g[4], o[4], rtol=1e-6, atol=1e-5, err_msg="t=%d" % t)
+        np.testing.assert_array_equal(g[3] != 0, o[3] != 0, err_msg="t=%d" % t)
+        if t >= meta["episode_length"] - 1:
+            assert g[5].all()                    # past the end: every agent done, no reset
+    assert not gpu.t_reset.cpu().numpy().any()
+    gpu.close()
