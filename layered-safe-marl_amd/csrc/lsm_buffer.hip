@@ -61,7 +61,14 @@ __global__ __launch_bounds__(256) void insert_kernel(InsertArgs a) {
   if (a.centralized) {
     const int row = N * OBS;
     float* so = a.share_obs + e0 * row;
-    for (int q = lane; q < N * row; q += WAVE) so[q] = o[q % row];
+    if ((row & 3) == 0) {   // 16-B rows (N * OBS % 4 == 0, e.g. 8 x 7): float4 copies
+      const int row4 = row >> 2;
+      const float4* o4 = (const float4*)o;
+      float4* so4 = (float4*)so;
+      for (int q = lane; q < N * row4; q += WAVE) so4[q] = o4[q % row4];
+    } else {
+      for (int q = lane; q < N * row; q += WAVE) so[q] = o[q % row];
+    }
     int32_t* sa = a.share_agent_id + e0 * N;
     for (int q = lane; q < N * N; q += WAVE) sa[q] = q % N;
   } else {
