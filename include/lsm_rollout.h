@@ -58,7 +58,12 @@ enum {
   LSM_OUT_DEBUG_STAMPS = 10, /* uint64 [n][16] per-phase clock stamps (diagnostic build only) */
   LSM_OUT_ADJ_MASK = 11,  /* uint64  [n][N][W] per-ego disconnect bits, W = ceil(E/64)
                              (adj_layout 1 only): bit r of ego e = entity r masked      */
-  LSM_NUM_OUT = 12
+  /* optional replay-buffer rows (GMPERunner.insert, graph_mpe_runner.py:457-481), written only
+     when bound: */
+  LSM_OUT_SHARE_OBS = 12, /* float32 [n][N][N*OBS] centralized share_obs (obs row per agent) */
+  LSM_OUT_MASKS = 13,     /* float32 [n][N]   1 - done                                   */
+  LSM_OUT_ACTIVE_MASKS = 14, /* float32 [n][N] done ? all(env dones) : 1                 */
+  LSM_NUM_OUT = 15
 };
 
 /* Adjacency output layouts (lsm_config.adj_layout).

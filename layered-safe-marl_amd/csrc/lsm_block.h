@@ -493,6 +493,7 @@ __global__ __launch_bounds__(BT) void rollout_block_kernel(const KParams* __rest
     gptr(P.o.dones)[(size_t)env * N + tid] = my_done ? 1 : 0;
   }
   const bool all_done = __syncthreads_and(my_done);
+  write_masks(P, env, N, tid, my_done, all_done);
   STAMP(9);
 
   // ---- 9. graph outputs, or the auto-reset (whose outputs replace them) ---------------------

@@ -121,6 +121,9 @@ struct OutDev {
   uint8_t* edges;
   double* state;
   uint64_t* adjmask;   // LSM_OUT_ADJ_MASK (compact adjacency layout)
+  float* share_obs;    // LSM_OUT_SHARE_OBS (optional)
+  float* masks;        // LSM_OUT_MASKS (optional)
+  float* active_masks; // LSM_OUT_ACTIVE_MASKS (optional)
 };
 
 struct KParams {
@@ -1410,28 +1413,49 @@ __device__ __forceinline__ void write_obs(const KParams& P, const Lds& S, int en
   LSM_DIMS;
   const int gi = goal_index(S.rpre[i], i, N, NL);
   const double gx = S.lm[gi], gy = S.lm[NL + gi], gh = S.lm[2 * NL + gi], gs = S.lm[3 * NL + gi];
-  GAS float* o = gptr(P.o.obs) + ((size_t)env * N + i) * (DYN ? 6 : 7);
+  constexpr int OB = DYN ? 6 : 7;
+  GAS float* o = gptr(P.o.obs) + ((size_t)env * N + i) * OB;
   const double px = S.ps[i], py = S.ps[N + i];
+  float v[OB];
   if (DYN == 0) {
-    o[0] = (float)S.ps[2 * N + i];
-    o[1] = (float)S.ps[3 * N + i];
-    o[2] = (float)(gx - px);
-    o[3] = (float)(gy - py);
-    o[4] = (float)S.lmsc[gi];
-    o[5] = (float)S.lmsc[NL + gi];
-    o[6] = (float)gs;
+    v[0] = (float)S.ps[2 * N + i];
+    v[1] = (float)S.ps[3 * N + i];
+    v[2] = (float)(gx - px);
+    v[3] = (float)(gy - py);
+    v[4] = (float)S.lmsc[gi];
+    v[5] = (float)S.lmsc[NL + gi];
+    v[DYN ? 5 : 6] = (float)gs;
   } else {
     const double th = S.ps[2 * N + i];
     double rx, ry;
     blas_rot(cos(th), sin(th), gx - px, gy - py, rx, ry);
     const double rh = gh - th;
-    o[0] = (float)S.ps[3 * N + i];
-    o[1] = (float)rx;
-    o[2] = (float)ry;
-    o[3] = (float)sin(rh);
-    o[4] = (float)cos(rh);
-    o[5] = (float)gs;
+    v[0] = (float)S.ps[3 * N + i];
+    v[1] = (float)rx;
+    v[2] = (float)ry;
+    v[3] = (float)sin(rh);
+    v[4] = (float)cos(rh);
+    v[5] = (float)gs;
   }
+#pragma unroll
+  for (int f = 0; f < OB; ++f) o[f] = v[f];
+  // LSM_OUT_SHARE_OBS (optional): GMPERunner.insert's centralized share_obs
+  // (graph_mpe_runner.py:469-481): the env's obs row repeated for every agent k
+  if (P.o.share_obs) {
+    GAS float* so = gptr(P.o.share_obs) + (size_t)env * N * N * OB + (size_t)i * OB;
+    for (int k = 0; k < N; ++k)
+#pragma unroll
+      for (int f = 0; f < OB; ++f) so[(size_t)k * N * OB + f] = v[f];
+  }
+}
+
+// LSM_OUT_MASKS / LSM_OUT_ACTIVE_MASKS (optional): GMPERunner.insert (graph_mpe_runner.py:457-467)
+// masks = !done; active_masks = done ? all(dones of the env) : 1
+__device__ __forceinline__ void write_masks(const KParams& P, int env, int N, int i, bool my_done, bool all_done) {
+  if (i >= N) return;
+  const size_t k = (size_t)env * N + i;
+  if (P.o.masks) gptr(P.o.masks)[k] = my_done ? 0.0f : 1.0f;
+  if (P.o.active_masks) gptr(P.o.active_masks)[k] = my_done ? (all_done ? 1.0f : 0.0f) : 1.0f;
 }
 
 // save_summary_of_episode (environment.py:895-911) from the LDS copy of the stats.
@@ -2057,6 +2081,7 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams* __restrict__
     gptr(P.o.dones)[(size_t)env * N + i] = my_done ? 1 : 0;
   }
   const bool all_done = group_all<LPE>(my_done);
+  write_masks(P, env, N, lane, my_done, all_done);
   if (chunked && !(P.auto_reset && all_done)) emit_adj_uniform<LPE, NT>(P, S, env, m_pre, 3 * N / 4, N);
   __syncthreads();
   STAMP(9);
@@ -2220,6 +2245,9 @@ static void fill_params(const lsm_env* e, KParams& P) {
   P.o.edges = (uint8_t*)e->out_ptr[LSM_OUT_EDGES];
   P.o.state = (double*)e->out_ptr[LSM_OUT_STATE];
   P.o.adjmask = (uint64_t*)e->out_ptr[LSM_OUT_ADJ_MASK];
+  P.o.share_obs = (float*)e->out_ptr[LSM_OUT_SHARE_OBS];
+  P.o.masks = (float*)e->out_ptr[LSM_OUT_MASKS];
+  P.o.active_masks = (float*)e->out_ptr[LSM_OUT_ACTIVE_MASKS];
   P.stamps = (unsigned long long*)e->out_ptr[LSM_OUT_DEBUG_STAMPS];
   P.diag = 0;
 #ifdef LSM_STAMPS
@@ -2245,6 +2273,9 @@ size_t lsm_output_bytes(const lsm_env* e, int32_t slot) {
     case LSM_OUT_EDGES: return n * E * E;
     case LSM_OUT_STATE: return n * N * 4 * 8;
     case LSM_OUT_DEBUG_STAMPS: return n * 16 * 8;
+    case LSM_OUT_SHARE_OBS: return n * N * N * e->OBS * 4;
+    case LSM_OUT_MASKS: return n * N * 4;
+    case LSM_OUT_ACTIVE_MASKS: return n * N * 4;
     default: return 0;
   }
 }
@@ -2536,6 +2567,9 @@ static void apply_ring(const lsm_env* e, int i, KParams& P) {
   P.o.info = (double*)at(LSM_OUT_INFO, P.o.info);
   P.o.state = (double*)at(LSM_OUT_STATE, P.o.state);
   P.o.adjmask = (uint64_t*)at(LSM_OUT_ADJ_MASK, P.o.adjmask);
+  P.o.share_obs = (float*)at(LSM_OUT_SHARE_OBS, P.o.share_obs);
+  P.o.masks = (float*)at(LSM_OUT_MASKS, P.o.masks);
+  P.o.active_masks = (float*)at(LSM_OUT_ACTIVE_MASKS, P.o.active_masks);
 }
 
 extern "C++" template <int DYN, int LPE, int NT>

@@ -8,9 +8,10 @@ dtypes, as torch tensors on the env's GPU) and the env-side halves of ``GMPERunn
 
 The rollout kernel writes obs / node_obs / adj into row t+1 and rewards into row t directly: the
 env's output slots are ring-bound to the buffer (``lsm_bind_output_ring``), one ring index per
-buffer row, so selecting a row is a host-side pointer choice. ``lsm_buffer_insert`` (HIP) then
-derives masks / active_masks / share_obs / share_agent_id / agent_id for that row from the step's
-obs and dones. Policy-side fields (rnn states, actions, values, log-probs) stay with the learner.
+buffer row, so selecting a row is a host-side pointer choice. With a centralized critic
+(``use_centralized_V``, the reference default) the kernel also writes that row's share_obs, masks and
+active_masks (optional output slots); otherwise ``lsm_buffer_insert`` (HIP) derives them from the
+step's obs and dones. agent_id / share_agent_id rows are constant and filled once. Policy-side fields (rnn states, actions, values, log-probs) stay with the learner.
 """
 from __future__ import annotations
 
@@ -50,6 +51,14 @@ class DeviceGraphBuffer:
         self.bad_masks = torch.ones_like(self.masks)
         self.active_masks = torch.ones_like(self.masks)
         self.step = 0
+        # agent ids are the same every row (the env returns agent index j for agent j)
+        ids = torch.arange(N, dtype=i32, device=dev)
+        self.agent_id.copy_(ids.view(1, 1, N, 1).expand_as(self.agent_id))
+        self.share_agent_id.copy_((ids.view(1, 1, 1, N) if self.centralized else ids.view(1, 1, N, 1))
+                                  .expand_as(self.share_agent_id))
+        # centralized critic: the rollout kernel also writes share_obs / masks / active_masks rows
+        # (LSM_OUT_SHARE_OBS / _MASKS / _ACTIVE_MASKS); otherwise lsm_buffer_insert derives them
+        self.fused = self.centralized
         self._bind()
         # per-row kernel arguments, built once (the per-step host path is two ctypes calls)
         self._rows = [tuple(C.c_void_p(t[r].data_ptr()) for t in (self.obs, self.share_obs, self.agent_id,
@@ -64,6 +73,9 @@ class DeviceGraphBuffer:
                  (capi.OUT_ADJ, self.adj, 0), (capi.OUT_REWARD, self.rewards, -1)]
         if self.adj_mask is not None:
             rings.append((capi.OUT_ADJ_MASK, self.adj_mask, 0))
+        if self.fused:
+            rings += [(capi.OUT_SHARE_OBS, self.share_obs, 0), (capi.OUT_MASKS, self.masks, 0),
+                      (capi.OUT_ACTIVE_MASKS, self.active_masks, 0)]
         for slot, t, off in rings:
             stride = t[0].numel() * t.element_size()
             capi.check(self.lib.lsm_bind_output_ring(self.env.h, slot, C.c_void_p(t.data_ptr()), stride,
@@ -71,7 +83,8 @@ class DeviceGraphBuffer:
 
     def detach(self):
         """Unbind the rings: the env writes its own output tensors again."""
-        for slot in (capi.OUT_OBS, capi.OUT_NODE_OBS, capi.OUT_ADJ, capi.OUT_REWARD, capi.OUT_ADJ_MASK):
+        for slot in (capi.OUT_OBS, capi.OUT_NODE_OBS, capi.OUT_ADJ, capi.OUT_REWARD, capi.OUT_ADJ_MASK,
+                     capi.OUT_SHARE_OBS, capi.OUT_MASKS, capi.OUT_ACTIVE_MASKS):
             capi.check(self.lib.lsm_bind_output_ring(self.env.h, slot, None, 0, 0, 0), self.env.h)
         capi.check(self.lib.lsm_select_ring(self.env.h, -1), self.env.h)
 
@@ -90,7 +103,8 @@ class DeviceGraphBuffer:
         """GMPERunner.warmup (graph_mpe_runner.py:253-283): reset into row 0. Returns ep_info."""
         self._select(0)
         ep = self.env.reset(num_current_episode)[-1]
-        self._insert(0, False)
+        if not self.fused:
+            self._insert(0, False)
         self.step = 0
         return ep
 
@@ -102,7 +116,8 @@ class DeviceGraphBuffer:
         self._select(t + 1)
         self.env.step_async(actions, num_current_episode)
         self.env.step_wait()
-        self._insert(t + 1, True)
+        if not self.fused:
+            self._insert(t + 1, True)
         self.step = (t + 1) % self.T
         return self.env.t_done, (self.env.t_info, self.env.t_reset, self.env.t_epinfo)
 

@@ -16,8 +16,8 @@ LIB_PATH = os.environ.get("LSM_LIB") or os.path.join(os.path.dirname(_HERE), "cs
 LSM_DOUBLE_INTEGRATOR, LSM_AIRTAXI = 0, 1
 LSM_ACTIONS_INDEX_I32, LSM_ACTIONS_ONEHOT_F32, LSM_ACTIONS_ONEHOT_F64 = 0, 1, 2
 (OUT_OBS, OUT_NODE_OBS, OUT_ADJ, OUT_REWARD, OUT_DONE, OUT_RESET_FLAG, OUT_EP_INFO, OUT_INFO,
- OUT_EDGES, OUT_STATE, OUT_DEBUG_STAMPS, OUT_ADJ_MASK) = range(12)
-NUM_OUT = 12
+ OUT_EDGES, OUT_STATE, OUT_DEBUG_STAMPS, OUT_ADJ_MASK, OUT_SHARE_OBS, OUT_MASKS, OUT_ACTIVE_MASKS) = range(15)
+NUM_OUT = 15
 ADJ_REFERENCE, ADJ_COMPACT = 0, 1
 INFO_FIELDS = ("individual_reward", "min_relative_distance", "Dist_to_goal", "Time_req_to_goal",
                "Num_agent_collisions", "Distance_mean", "Distance_variance", "Dists_traveled",

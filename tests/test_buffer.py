@@ -68,8 +68,8 @@ def test_gpu_insert_rows(n, N, OBS, centralized):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("layout", ["reference", "compact"])
-def test_gpu_buffer_rollout_matches_plain_env(layout):
+@pytest.mark.parametrize("layout,centralized", [("reference", True), ("compact", True), ("reference", False)])
+def test_gpu_buffer_rollout_matches_plain_env(layout, centralized):
     """warmup + 2.5 episodes with auto-resets and after_update: the ring-bound buffer rows equal a
     plainly bound env's outputs on the same seeds and actions, and the derived rows equal the
     oracle's insert of those outputs."""
@@ -84,7 +84,8 @@ def test_gpu_buffer_rollout_matches_plain_env(layout):
     mk = lambda: GpuGraphVecEnv(args, num_envs=n, device="cuda:0", value_table=vt, return_numpy=False,
                                 build_infos=False, adj_layout=layout)
     plain, ringed = mk(), mk()
-    buf = DeviceGraphBuffer(ringed, episode_length=T)
+    buf = DeviceGraphBuffer(ringed, episode_length=T, use_centralized_V=centralized)
+    assert buf.fused == centralized   # kernel-written rows (centralized) or the insert kernel
     plain.reset(4)
     buf.warmup(4)
     aid = np.tile(np.arange(8).reshape(1, 8, 1), (n, 1, 1))
@@ -95,7 +96,7 @@ def test_gpu_buffer_rollout_matches_plain_env(layout):
         np.testing.assert_array_equal(buf.adj[row].cpu().numpy(), plain.t_adj.cpu().numpy())
         if layout == "compact":
             np.testing.assert_array_equal(buf.adj_mask[row].cpu().numpy(), plain.t_adj_mask.cpu().numpy())
-        want = insert_rows(plain.t_obs.cpu().numpy(), aid, dones, True)
+        want = insert_rows(plain.t_obs.cpu().numpy(), aid, dones, centralized)
         for k, v in want.items():
             np.testing.assert_array_equal(getattr(buf, k)[row].cpu().numpy(), v, err_msg=k)
 
