@@ -20,6 +20,11 @@
  *                        MultiAgentGraphEnv.step (environment.py:963-1042) incl. the
  *                        worker's auto-reset on np.all(done) (env_wrappers.py:866-871)
  *   lsm_last_error       exception text (Python wrapper raises RuntimeError)
+ *   lsm_bind_output_ring / lsm_select_ring
+ *                        outputs written in place into GraphReplayBuffer rows
+ *                        (graph_mpe_runner.py:444-487, graph_buffer.py:223-249)
+ *   lsm_edges_*          GNNBase.process_adj (onpolicy/algorithms/utils/gnn.py:376-407)
+ *   lsm_buffer_insert    GMPERunner.insert's derived rows (graph_mpe_runner.py:449-484)
  *
  * Kernels: N <= 32 and N * (1 + L) <= 64 run one 64-lane wavefront per env; larger envs
  * (up to N = 64, E = 256: BASELINE config 5) one 256-thread workgroup per env.
