@@ -181,7 +181,7 @@ template <int DYN, int NT>
 __global__ __launch_bounds__(BT) void rollout_block_kernel(const KParams* __restrict__ Pp, const KStep K) {
   const KParams& P = *Pp;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int env = blockIdx.x;
+  const int env = xcd_block(blockIdx.x, gridDim.x);
   const int tid = threadIdx.x;
   const int lane = tid;   // (STAMP macros)
   if (env >= P.n_envs) return;   // uniform over the workgroup

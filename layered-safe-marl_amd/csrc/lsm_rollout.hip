@@ -1449,6 +1449,17 @@ __device__ __forceinline__ void write_obs(const KParams& P, const Lds& S, int en
   }
 }
 
+// Workgroup -> env block. Workgroups are dispatched round-robin over the 8 XCDs (wg b on XCD b % 8).
+// With LSM_XCD_REMAP each XCD takes one contiguous range of envs, so the output rows an XCD's L2
+// writes back are contiguous (neighbouring envs' rows share cache lines: obs rows are 224 B).
+__device__ __forceinline__ int xcd_block(int b, int nb) {
+#ifdef LSM_XCD_REMAP
+  if ((nb & 7) == 0) return (b & 7) * (nb >> 3) + (b >> 3);
+#endif
+  (void)nb;
+  return b;
+}
+
 // LSM_OUT_MASKS / LSM_OUT_ACTIVE_MASKS (optional): GMPERunner.insert (graph_mpe_runner.py:457-467)
 // masks = !done; active_masks = done ? all(dones of the env) : 1
 __device__ __forceinline__ void write_masks(const KParams& P, int env, int N, int i, bool my_done, bool all_done) {
@@ -1868,7 +1879,7 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams* __restrict__
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int G = WAVE / LPE;   // envs per wave, one per LPE-lane group
   const int grp = (G == 1) ? 0 : (int)threadIdx.x / LPE;
-  const int env = blockIdx.x * G + grp;
+  const int env = xcd_block(blockIdx.x, gridDim.x) * G + grp;
   const int lane = threadIdx.x & (LPE - 1);
   if (env >= P.n_envs) return;
   LSM_DIMS;
