@@ -212,7 +212,9 @@ int make_src(const float* adj, const uint64_t* masks, int64_t B, int32_t E, int3
 
 size_t scan_temp_bytes(int64_t B) {
   size_t bytes = 0;
-  hipcub::DeviceScan::InclusiveSum(nullptr, bytes, (const int64_t*)nullptr, (int64_t*)nullptr, (int)B);
+  if (hipcub::DeviceScan::InclusiveSum(nullptr, bytes, (const int64_t*)nullptr, (int64_t*)nullptr, (int)B) !=
+      hipSuccess)
+    return 0;   // lsm_edges_count then reports "scan failed"
   return bytes;
 }
 
