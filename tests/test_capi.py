@@ -109,3 +109,14 @@ def test_config_validation():
     with pytest.raises(ValueError):
         EnvArgs(num_env_steps=10).validate()
     EnvArgs().validate()
+
+
+def test_header_is_plain_c_abi():
+    """include/lsm_rollout.h compiles as C99 and C++11 on its own: no torch or HIP types at the boundary."""
+    import shutil
+    import subprocess
+    hdr = os.path.join(ROOT, "include", "lsm_rollout.h")
+    for cc, std, lang in (("gcc", "-std=c99", "c"), ("g++", "-std=c++11", "c++")):
+        if shutil.which(cc) is None:
+            pytest.skip("%s not available" % cc)
+        subprocess.check_call([cc, std, "-Wall", "-Wextra", "-Werror", "-fsyntax-only", "-x", lang, hdr])
