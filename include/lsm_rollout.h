@@ -128,10 +128,17 @@ void lsm_destroy(lsm_env* env);
 const char* lsm_last_error(const lsm_env* env);
 
 /* values: float32 [prod(shape)] (values_hj, already negated/shifted); grads: float32
- * [prod(shape)][gwidth] with gwidth = 4 (ndim <= 4) or 8 (ndim == 5); periodic: 0/1 per dim. */
+ * [prod(shape)][gwidth] with gwidth = 4 (ndim <= 4) or 8 (ndim == 5); periodic: 0/1 per dim.
+ * separation_distance: the separation values_hj is calibrated for (HjDataHandle's
+ * target_separation_distance, safety_filter.py:155-168). Each env then keeps its own table
+ * history: every reset whose curriculum separation differs from the env's current one applies
+ * `values_hj -= shift` (float32 <- float64, HjDataHandle.update_separation_distance,
+ * safety_filter.py:170-174) to that env only. At most 8 separation changes across the
+ * reset/step calls' curriculum blocks are accepted per upload (lsm_step / lsm_reset fail
+ * beyond that); uploading again starts every env's history afresh. */
 int lsm_set_value_table(lsm_env* env, int32_t ndim, const double* lo, const double* hi,
                         const int32_t* shape, const int32_t* periodic,
-                        const float* values_host, const float* grads_host);
+                        const float* values_host, const float* grads_host, double separation_distance);
 int lsm_set_ttr_table(lsm_env* env, int32_t ndim, const double* lo, const double* hi,
                       const int32_t* shape, const int32_t* periodic,
                       const float* values_host, double ttr_max);
@@ -169,6 +176,11 @@ int32_t lsm_obs_dim(const lsm_env* env);        /* OBS */
 /* Host-side entry points of the SAME scenario-generation / RNG code the reset kernel runs
  * (no GPU needed): used by CPU tests against numpy's legacy RandomState. */
 int lsm_host_mt_uniforms(uint32_t seed, int32_t count, double lo, double hi, double* out);
+/* The double integrator's step as the kernel computes it: scipy's solve_ivp(x' = v, v' = a,
+ * [0, dt], y0, 'RK45').y[:, -1] restated operation for operation (core.py:199-210); returns the
+ * number of RK45 steps. lsm_host_glibc_pow: the kernel's restatement of glibc's pow. */
+int lsm_host_rk45_di(const double* y0 /* [4] */, double a0, double a1, double dt, double* y_out /* [4] */);
+double lsm_host_glibc_pow(double x, double y);
 int lsm_host_scenario(const lsm_config* cfg, const lsm_curriculum* cur, uint32_t seed,
                       double* agent_state /* [N][4] */, double* landmarks /* [NL][4] */);
 

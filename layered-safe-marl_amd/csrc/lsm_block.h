@@ -255,6 +255,7 @@ __global__ __launch_bounds__(BT) void rollout_block_kernel(const KParams* __rest
   // so the argmin (first occurrence on ties) and its value are exactly the full search's.
   const bool filter_on = S.cur[C_FILT] != 0.0;
   if (filter_on) {
+    const SepChain sc = sep_chain(S.sep);
     const int i = tid / TE, q = tid - (tid / TE) * TE;
     int jd = -1, jv = -1, okv = 0;
     double dmin = 0.0;
@@ -276,7 +277,7 @@ __global__ __launch_bounds__(BT) void rollout_block_kernel(const KParams* __rest
           double rel[5];
           rel_state<DYN>(S, N, i, j, rel);
           float2 b;
-          if (DYN == 0 ? value_bounds<4>(P.val, rel, b) : value_bounds<5>(P.val, rel, b)) {
+          if (DYN == 0 ? value_bounds<4>(P.val, rel, b, sc) : value_bounds<5>(P.val, rel, b, sc)) {
             lbk[k] = b.x;
             ub = fminf(ub, b.y);
           } else {
@@ -323,7 +324,7 @@ __global__ __launch_bounds__(BT) void rollout_block_kernel(const KParams* __rest
         double rel[5];
         rel_state<DYN>(S, N, ii, jj, rel);
         float v = 0.0f;
-        const bool ok = DYN == 0 ? interp_value<4>(P.val, rel, v) : interp_value<5>(P.val, rel, v);
+        const bool ok = DYN == 0 ? interp_value<4>(P.val, rel, v, sc) : interp_value<5>(P.val, rel, v, sc);
         qv[x] = ok ? v : __builtin_nanf("");
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -357,7 +358,7 @@ __global__ __launch_bounds__(BT) void rollout_block_kernel(const KParams* __rest
           rel_state<DYN>(S, N, i, j, rel);
           float v = 0.0f;
           bool ok;
-          if (DYN == 0) ok = interp_value<4>(P.val, rel, v); else ok = interp_value<5>(P.val, rel, v);
+          if (DYN == 0) ok = interp_value<4>(P.val, rel, v, sc); else ok = interp_value<5>(P.val, rel, v, sc);
           if (!ok) v = INFINITY;
           if (jd < 0 || d < dmin) { jd = j; dmin = d; }
           if (jv < 0 || v < vmin) { jv = j; vmin = v; okv = ok ? 1 : 0; }

@@ -35,6 +35,7 @@
 
 #include "../../include/lsm_rollout.h"
 #include "lsm_numeric.h"
+#include "lsm_rk45.h"
 #include "lsm_scenario.h"
 
 #ifdef LSM_STAMPS
@@ -69,6 +70,13 @@ constexpr int MT_WORDS = MT_N + 1;  // key[624] + pos
 constexpr int NCUR = 12;
 constexpr int NSTAT = 6;        // travel_length, travel_distance, done, conflict, min_distance, multiple
 constexpr int NWINFO = 4;       // times_required, dists_to_goal, dist_left_to_goal, num_agent_collisions
+// Per-env HJ separation history (record, after cur): HjDataHandle.update_separation_distance
+// (safety_filter.py:170-174) runs `values_hj -= shift` on every reset of every env, so each env's
+// table is the uploaded one minus its own chain of float64 shifts, each rounded to float32
+// (numpy: float32 array -= float64 scalar). sep[0] = number of shifts, sep[1] = the env's current
+// separation (sep[0] == 0: the uploaded table's, KParams::val_sep0), sep[2 + k] = shift k.
+constexpr int KSEP = 8;
+constexpr int NSEPW = 2 + KSEP;
 
 // HJ / TTR table in "cell-corner" layout: every grid cell stores the 2^ndim corner values
 // it interpolates (lexicographic corner order, dim 0 slowest) contiguously, so one query
@@ -139,6 +147,7 @@ struct KParams {
   double at_vmax, at_vmin, at_amax, at_amin, at_wmax, at_thr_amax, at_thr_amin;
   float at_box_w, at_box_amax, at_box_amin;  // float32 box corners (jnp)
   double ttr_max;
+  double val_sep0;       // separation of the uploaded value table (HjDataHandle.separation_distance)
   uint32_t m_E, m_EE, m_EF, m_F, m_EF4, m_NL;  // ceil(2^32 / d) for exact small-numerator division
   unsigned long long* stamps;     // LSM_OUT_DEBUG_STAMPS (diagnostic builds only)
   int diag;                       // diagnostic builds: bit 0 skip adj/node stores, bit 1 skip filter (LSM_DIAG)
@@ -177,6 +186,7 @@ struct Lds {
   int32_t* decon;    // [N]
   int32_t* step;     // [2] env.current_step; 1 = cached distances unmasked (state edited)
   double* cur;       // [NCUR]
+  double* sep;       // [NSEPW] HJ separation shift chain (= cur + NCUR)
   double* lm;        // [6][NL] x, y, heading, speed, sin, cos
   double* lmsc;      // = lm + 4 NL
   float* lmd;        // [NL(NL-1)/2] thresholded landmark-landmark distances (per episode)
@@ -291,7 +301,7 @@ __host__ __device__ inline LdsPlan lds_plan(int N, int NL, int E, int F, bool bl
   put(8 * N); put(8 * N); put(8 * N); put(8 * N);
   put(4 * N); put(4 * N); put(4 * N); put(4 * N); put(8);
   p.hot = o;
-  put(8 * NCUR); put(8 * 6 * NL); put(block ? 0 : 4 * (NL * (NL - 1) / 2));
+  put(8 * (NCUR + NSEPW)); put(8 * 6 * NL); put(block ? 0 : 4 * (NL * (NL - 1) / 2));
   p.rec = o;
   const int MW = (E + 63) / 64;
   // scratch
@@ -367,6 +377,7 @@ __device__ __forceinline__ Lds carve(unsigned char* base, int N, int NL, int E, 
   L.decon = (int32_t*)(base + p.off[k++]);
   L.step = (int32_t*)(base + p.off[k++]);
   L.cur = (double*)(base + p.off[k++]);
+  L.sep = L.cur + NCUR;
   L.lm = (double*)(base + p.off[k++]);
   L.lmsc = L.lm + 4 * NL;
   L.lmd = (float*)(base + p.off[k++]);
@@ -414,6 +425,7 @@ __device__ __forceinline__ Lds carve_block(unsigned char* base, int N, int NL, i
   L.decon = (int32_t*)(base + p.off[k++]);
   L.step = (int32_t*)(base + p.off[k++]);
   L.cur = (double*)(base + p.off[k++]);
+  L.sep = L.cur + NCUR;
   L.lm = (double*)(base + p.off[k++]);
   L.lmsc = L.lm + 4 * NL;
   L.lmd = nullptr; k++;
@@ -552,8 +564,27 @@ __device__ __forceinline__ bool grid_cell(const TableDev& T, const double* s, in
   return true;
 }
 
+// One env's chain of separation shifts (Lds::sep): node values are the uploaded ones minus
+// each shift in turn, float64 subtraction rounded to float32 (`values_hj -= shift`,
+// safety_filter.py:173, a float32 array minus a numpy float64 scalar).
+struct SepChain {
+  const double* sh;   // shifts in application order
+  int n;
+  __device__ __forceinline__ float apply(float v) const {
+    for (int k = 0; k < n; ++k) v = (float)((double)v - sh[k]);
+    return v;
+  }
+};
+__device__ __forceinline__ SepChain sep_chain(const double* sep) {
+  SepChain c;
+  c.n = (int)sep[0];
+  c.sh = sep + 2;
+  return c;
+}
+
 template <int ND>
-__device__ __forceinline__ bool interp_value(const TableDev& T, const double* s, float& out) {
+__device__ __forceinline__ bool interp_value(const TableDev& T, const double* s, float& out,
+                                             SepChain sc = SepChain{nullptr, 0}) {
   int cell;
   float w[1 << ND];
   if (!grid_cell<ND>(T, s, cell, w)) return false;
@@ -563,6 +594,10 @@ __device__ __forceinline__ bool interp_value(const TableDev& T, const double* s,
   for (int q = 0; q < (1 << ND) / 4; ++q) {
     const f32x4 x = c4[q];
     v[4 * q] = x.x; v[4 * q + 1] = x.y; v[4 * q + 2] = x.z; v[4 * q + 3] = x.w;
+  }
+  if (sc.n > 0) {
+#pragma unroll
+    for (int c = 0; c < (1 << ND); ++c) v[c] = sc.apply(v[c]);
   }
   float acc = 0.0f;
 #pragma unroll
@@ -598,7 +633,8 @@ __device__ __forceinline__ void interp_grad(const TableDev& T, const double* s, 
 // its cell. Same in-range decision and cell index as grid_cell(); false = out of the grid
 // (the lookup is +inf, no load).
 template <int ND>
-__device__ __forceinline__ bool value_bounds(const TableDev& T, const double* s, float2& b) {
+__device__ __forceinline__ bool value_bounds(const TableDev& T, const double* s, float2& b,
+                                             SepChain sc = SepChain{nullptr, 0}) {
   int blk = 0;
 #pragma unroll
   for (int d = 0; d < ND; ++d) {
@@ -619,6 +655,13 @@ __device__ __forceinline__ bool value_bounds(const TableDev& T, const double* s,
   typedef float f32x2 __attribute__((ext_vector_type(2)));
   const f32x2 x = *((const GAS f32x2*)gptr(T.bnd) + blk);
   b = make_float2(x.x, x.y);
+  if (sc.n > 0) {
+    // the shift chain is monotone, so the shifted corners stay within the shifted bounds;
+    // widen again for the interpolation error at the shifted magnitude (bounds_kernel)
+    const float lo = sc.apply(b.x), hi = sc.apply(b.y);
+    const float m = 4.0e-6f * fmaxf(fabsf(lo), fabsf(hi));
+    b = make_float2(lo - m, hi + m);
+  }
   return true;
 }
 
@@ -1556,6 +1599,20 @@ __device__ __forceinline__ void reset_core(const KParams& P, Lds& S, int env, co
   }
   __syncthreads();
   for (int k = lane; k < NCUR; k += LPE) S.cur[k] = cur_new[k];
+  if (lane == 0 && P.use_filter_arg) {
+    // update_curriculum -> world.update_safety_filter_separation_distance -> HjDataHandle.
+    // update_separation_distance (navigation_graph_safe.py:363-364, core.py:483-486,
+    // safety_filter.py:170-174): shift = target - previous in float64; a zero shift leaves the
+    // table unchanged. The host bounds the chain length (lsm_step / lsm_reset refuse > KSEP).
+    const int n = (int)S.sep[0];
+    const double prev = n ? S.sep[1] : P.val_sep0;
+    const double sh = cur_new[C_SEP] - prev;
+    if (sh != 0.0 && n < KSEP) {
+      S.sep[2 + n] = sh;
+      S.sep[0] = (double)(n + 1);
+      S.sep[1] = cur_new[C_SEP];
+    }
+  }
   const GAS uint32_t* mtg = gptr(P.s.mt) + (size_t)env * MT_WORDS;
   for (int k = lane; k < MT_WORDS; k += LPE) S.mt[k] = mtg[k];
   __syncthreads();
@@ -1649,7 +1706,9 @@ __device__ __forceinline__ void store_state(const KParams& P, Lds& S, const unsi
   rec_copy<LPE>((const f32x4*)lbase, (GAS f32x4*)gptr(P.s.rec) + (size_t)env * P.s.rec_stride16, full ? P.s.rec16 : P.s.hot16);
 }
 
-// closed-form integration of agent i, speed clamp, travel distance (core.py:118-131,199-210,680-687)
+// integration of agent i, speed clamp, travel distance (core.py:118-131,199-210,680-687):
+// the double integrator replays scipy's RK45 call operation for operation (lsm_rk45.h), airtaxi
+// uses a stable closed form (its RK45 right-hand side goes through numpy's SIMD cos / sin)
 template <int DYN>
 __device__ __forceinline__ void integrate_agent(const KParams& P, Lds& S, int N, int i) {
   const double dt = P.dt;
@@ -1657,10 +1716,9 @@ __device__ __forceinline__ void integrate_agent(const KParams& P, Lds& S, int N,
   double x = S.ps[i], y = S.ps[N + i], s2 = S.ps[2 * N + i], s3 = S.ps[3 * N + i];
   double spd;
   if (DYN == 0) {
-    x = x + s2 * dt + 0.5 * a0 * dt * dt;
-    y = y + s3 * dt + 0.5 * a1 * dt * dt;
-    s2 = s2 + a0 * dt;
-    s3 = s3 + a1 * dt;
+    double yv[4] = {x, y, s2, s3};
+    rk45_di(yv, a0, a1, dt);
+    x = yv[0]; y = yv[1]; s2 = yv[2]; s3 = yv[3];
     spd = sqrt(s2 * s2 + s3 * s3);
     if (spd > P.max_speed) {
       s2 = P.max_speed * s2 / spd;
@@ -1981,6 +2039,7 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams* __restrict__
   const bool filter_on = S.cur[C_FILT] != 0.0;
 #endif
   if (filter_on) {
+    const SepChain sc = sep_chain(S.sep);
     const int npairs = N * N;
     for (int p = lane; p < npairs; p += LPE) {
       const int i = p / N, j = p - i * N;
@@ -1991,7 +2050,7 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams* __restrict__
       rel_state<DYN>(S, N, i, j, rel);
       float v = 0.0f;
       bool ok;
-      if (DYN == 0) ok = interp_value<4>(P.val, rel, v); else ok = interp_value<5>(P.val, rel, v);
+      if (DYN == 0) ok = interp_value<4>(P.val, rel, v, sc); else ok = interp_value<5>(P.val, rel, v, sc);
       S.vpair[p] = ok ? v : INFINITY;
       S.inr[p] = ok ? 1 : 0;
     }
@@ -2118,6 +2177,15 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams* __restrict__
 
 #include "lsm_block.h"
 
+// A new value table (a new HjDataHandle): every env's separation chain starts empty.
+__global__ void sep_clear_kernel(float4* rec, uint32_t rec_stride16, int n_envs, uint32_t sep_off) {
+  const int env = blockIdx.x * blockDim.x + threadIdx.x;
+  if (env >= n_envs) return;
+  double* sep = (double*)((unsigned char*)(rec + (size_t)env * rec_stride16) + sep_off);
+  sep[0] = 0.0;
+  sep[1] = 0.0;
+}
+
 // env k's MT19937: np.random.seed(seed + 1000 * (env_offset + k))
 __global__ void seed_kernel(uint32_t* mt, int n_envs, int64_t seed, int64_t env_offset) {
   const int env = blockIdx.x * blockDim.x + threadIdx.x;
@@ -2145,6 +2213,9 @@ struct lsm_env {
   size_t out_bytes[LSM_NUM_OUT];
   TableDev val, ttr;
   double ttr_max;
+  double val_sep0;      // separation of the uploaded value table
+  double sep_last;      // separation of the last reset / step call (chain-length bound)
+  int sep_changes;      // changes of that separation since the table upload (>= any env's chain)
   std::string err;
   bool tables_ok;
   int device;
@@ -2242,6 +2313,7 @@ static void fill_params(const lsm_env* e, KParams& P) {
   P.m_EF4 = magic(e->E * e->F / 4);
   P.m_NL = magic(e->NL);
   P.ttr_max = e->ttr_max;
+  P.val_sep0 = e->val_sep0;
   P.val = e->val;
   P.ttr = e->ttr;
   P.s = e->s;
@@ -2310,6 +2382,8 @@ int lsm_create(const lsm_config* cfg, lsm_env** out) {
   e->ring_len = 0; e->ring_cap = 0; e->ring_sel = -1; e->dring = nullptr;
   e->params_dirty = true;
   e->ttr_max = 0.0;
+  e->val_sep0 = e->sep_last = 0.0;
+  e->sep_changes = 0;
   memset(&e->val, 0, sizeof(e->val));
   memset(&e->ttr, 0, sizeof(e->ttr));
   for (int k = 0; k < LSM_NUM_OUT; ++k) { e->out_ptr[k] = nullptr; e->out_bytes[k] = 0; }
@@ -2405,10 +2479,25 @@ void lsm_destroy(lsm_env* e) {
   delete e;
 }
 
+// Free one of the handle's allocations (a replaced table).
+static void dfree(lsm_env* e, const void* p) {
+  if (!p) return;
+  for (size_t k = 0; k < e->allocs.size(); ++k)
+    if (e->allocs[k] == p) {
+      (void)hipFree(e->allocs[k]);
+      e->allocs.erase(e->allocs.begin() + k);
+      return;
+    }
+}
+
 static int upload_table(lsm_env* e, TableDev& T, int32_t ndim, const double* lo, const double* hi,
                         const int32_t* shape, const int32_t* periodic, const float* values,
                         const float* grads) {
   if (ndim < 1 || ndim > 5) return fail(e, "table ndim must be in [1, 5]");
+  HIPCHK(e, hipDeviceSynchronize());   // a replaced table may still be read by queued launches
+  dfree(e, T.cells);
+  dfree(e, T.gcells);
+  dfree(e, T.bnd);
   memset(&T, 0, sizeof(T));
   T.ndim = ndim;
   size_t nodes = 1, cells = 1;
@@ -2481,12 +2570,23 @@ static int upload_bounds(lsm_env* e, TableDev& T, const float* values) {
 }
 
 int lsm_set_value_table(lsm_env* e, int32_t ndim, const double* lo, const double* hi, const int32_t* shape,
-                        const int32_t* periodic, const float* values, const float* grads) {
+                        const int32_t* periodic, const float* values, const float* grads,
+                        double separation_distance) {
   const int want = e->cfg.dynamics == LSM_DOUBLE_INTEGRATOR ? 4 : 5;
   if (ndim != want) return fail(e, "value table must be 4-D (double integrator) or 5-D (airtaxi)");
   if (!grads) return fail(e, "value table needs its gradient table");
   if (upload_table(e, e->val, ndim, lo, hi, shape, periodic, values, grads)) return 1;
   if (upload_bounds(e, e->val, values)) return 1;
+  e->val_sep0 = e->sep_last = separation_distance;
+  e->sep_changes = 0;
+  {
+    const LdsPlan lp = lds_plan(e->N, e->NL, e->E, e->F, e->block);
+    const int n = e->cfg.num_envs;
+    hipLaunchKernelGGL(sep_clear_kernel, dim3((n + 255) / 256), dim3(256), 0, 0, e->s.rec, e->s.rec_stride16, n,
+                       (uint32_t)(lp.off[12] + 8 * NCUR));
+    HIPCHK(e, hipGetLastError());
+    HIPCHK(e, hipDeviceSynchronize());
+  }
   e->tables_ok = (e->cfg.dynamics == LSM_DOUBLE_INTEGRATOR) || e->ttr.cells != nullptr;
   e->params_dirty = true;
   return 0;
@@ -2555,6 +2655,21 @@ static int check_ready(lsm_env* e, bool stepping) {
   if (e->cfg.adj_layout == LSM_ADJ_COMPACT && !e->out_ptr[LSM_OUT_ADJ_MASK])
     return fail(e, "compact adjacency layout needs LSM_OUT_ADJ_MASK bound");
   (void)stepping;
+  return 0;
+}
+
+// Every env's shift chain holds at most KSEP entries; an env's chain grows only at its resets,
+// by one entry per change of the separation it resets with, so the changes across the calls'
+// curriculum blocks since the table upload bound every chain.
+static int sep_check(lsm_env* e, const lsm_curriculum* cur) {
+  if (!e->cfg.use_safety_filter) return 0;
+  if (cur->separation_distance != e->sep_last) {
+    if (e->sep_changes + 1 > KSEP)
+      return fail(e, "more than " + std::to_string(KSEP) + " separation-distance changes since the value table "
+                     "was set (per-env HJ shift chain is bounded); re-upload the table");
+    e->sep_changes++;
+    e->sep_last = cur->separation_distance;
+  }
   return 0;
 }
 
@@ -2690,6 +2805,7 @@ int lsm_set_agent_state(lsm_env* e, int32_t env_index, const double* state, cons
 int lsm_reset(lsm_env* e, const lsm_curriculum* cur, void* stream) {
   if (!e || !cur) return 1;
   if (check_ready(e, false)) return 1;
+  if (sep_check(e, cur)) return 1;
   KStep L;
   memset(&L, 0, sizeof(L));
   memcpy(L.cur_new, cur, sizeof(double) * NCUR);
@@ -2702,6 +2818,7 @@ int lsm_step(lsm_env* e, const void* actions, int32_t kind, const lsm_curriculum
   if (!e || !actions || !cur) return fail(e, "null argument");
   if (kind < 0 || kind > 2) return fail(e, "bad action kind");
   if (check_ready(e, true)) return 1;
+  if (sep_check(e, cur)) return 1;
   KStep L;
   memcpy(L.cur_new, cur, sizeof(double) * NCUR);
   L.mode = 0;
@@ -2710,6 +2827,15 @@ int lsm_step(lsm_env* e, const void* actions, int32_t kind, const lsm_curriculum
   L.emit_edges = e->cfg.emit_edges && e->out_ptr[LSM_OUT_EDGES] != nullptr;
   return launch(e, L, (hipStream_t)stream);
 }
+
+int lsm_host_rk45_di(const double* y0, double a0, double a1, double dt, double* y_out) {
+  double y[4] = {y0[0], y0[1], y0[2], y0[3]};
+  const int n = rk45_di(y, a0, a1, dt);
+  for (int i = 0; i < 4; ++i) y_out[i] = y[i];
+  return n;
+}
+
+double lsm_host_glibc_pow(double x, double y) { return glibc_pow(x, y); }
 
 int lsm_host_mt_uniforms(uint32_t seed, int32_t count, double lo, double hi, double* out) {
   HostMT m;

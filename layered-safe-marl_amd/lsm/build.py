@@ -15,7 +15,7 @@ OUT = os.path.join(CSRC, "liblsm_rollout.so")
 HDR = os.path.join(os.path.dirname(os.path.dirname(HERE)), "include", "lsm_rollout.h")
 # translation units -> their dependencies (each compiled to its own object, then linked)
 UNITS = {
-    "lsm_rollout.hip": ["lsm_numeric.h", "lsm_scenario.h", "lsm_block.h"],
+    "lsm_rollout.hip": ["lsm_numeric.h", "lsm_scenario.h", "lsm_block.h", "lsm_rk45.h", "lsm_pow_tables.h"],
     "lsm_edges.hip": [],
     "lsm_buffer.hip": [],
 }

@@ -30,7 +30,7 @@ EXPORTED = ("lsm_create", "lsm_destroy", "lsm_last_error", "lsm_set_value_table"
             "lsm_node_features", "lsm_obs_dim", "lsm_host_mt_uniforms", "lsm_host_scenario",
             "lsm_set_agent_state", "lsm_edges_workspace_bytes", "lsm_edges_count", "lsm_edges_emit",
             "lsm_edges_last_error", "lsm_bind_output_ring", "lsm_select_ring", "lsm_buffer_insert",
-            "lsm_buffer_last_error")
+            "lsm_buffer_last_error", "lsm_host_rk45_di", "lsm_host_glibc_pow")
 
 
 class LsmConfig(C.Structure):
@@ -69,7 +69,7 @@ def load_library(path: str = LIB_PATH):
         "lsm_create": (I32, [C.POINTER(LsmConfig), C.POINTER(P)]),
         "lsm_destroy": (None, [P]),
         "lsm_last_error": (C.c_char_p, [P]),
-        "lsm_set_value_table": (I32, [P, I32, P, P, P, P, P, P]),
+        "lsm_set_value_table": (I32, [P, I32, P, P, P, P, P, P, D]),
         "lsm_set_ttr_table": (I32, [P, I32, P, P, P, P, P, D]),
         "lsm_bind_output": (I32, [P, I32, P, SZ]),
         "lsm_output_bytes": (SZ, [P, I32]),
@@ -89,6 +89,8 @@ def load_library(path: str = LIB_PATH):
         "lsm_select_ring": (I32, [P, I32]),
         "lsm_buffer_insert": (I32, [P, P, I32, I32, I32, I32, P, P, P, P, P, P]),
         "lsm_buffer_last_error": (C.c_char_p, []),
+        "lsm_host_rk45_di": (I32, [P, D, D, D, P]),
+        "lsm_host_glibc_pow": (D, [D, D]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

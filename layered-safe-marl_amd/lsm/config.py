@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import argparse
 from dataclasses import dataclass, asdict
+from typing import Optional
 
 import numpy as np
 
@@ -103,6 +104,19 @@ class EnvArgs:
     graph_feat_type: str = "relative"
     discrete_action: bool = True
     seed: int = 0
+    # RewardBinaryConfig.SEPARATION_DISTANCE_CURRICULUM (a hand-edited class constant in the
+    # reference, config.py:81); None = that constant, True / False override it per env handle
+    separation_distance_curriculum: Optional[bool] = None
+
+    def sep_curriculum(self) -> bool:
+        v = self.separation_distance_curriculum
+        return bool(RewardBinaryConfig.SEPARATION_DISTANCE_CURRICULUM if v is None else v)
+
+    def initial_separation(self) -> float:
+        """The scenario's separation_distance_init, which HjDataHandle is built with
+        (navigation_graph_safe.py:183-196, core.py:429,456)."""
+        C = DoubleIntegratorConfig if self.dynamics_type == "double_integrator" else AirTaxiConfig
+        return 0 if self.sep_curriculum() else C.SEPARATION_DISTANCE
 
     @staticmethod
     def from_namespace(ns: argparse.Namespace) -> "EnvArgs":

@@ -45,7 +45,8 @@ def curriculum_block(args, num_current_episode: int) -> dict:
     if (not (use_filter and RewardBinaryConfig.INITIAL_PHASE_USE_SAFETY_FILTER)) and use_filter:
         world_filter = bool(sl > 0)
     sep_t = C.SEPARATION_DISTANCE
-    sep_i = 0 if RewardBinaryConfig.SEPARATION_DISTANCE_CURRICULUM else sep_t
+    sep_i = args.initial_separation() if hasattr(args, "initial_separation") else (
+        0 if RewardBinaryConfig.SEPARATION_DISTANCE_CURRICULUM else sep_t)
     sep = sep_i * (1.0 - rsd) + sep_t * rsd
     eng = C.ENGAGEMENT_DISTANCE + (sep - C.ENGAGEMENT_DISTANCE_REFERENCE_SEPARATION_DISTANCE)
     cra = 1 if use_filter else _sloped(r, start=0.25, end=0.75)

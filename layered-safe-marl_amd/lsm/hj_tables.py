@@ -53,14 +53,6 @@ class HjTable:
             per[d] = True
         return np.where(per, (self.hi - self.lo) / n, (self.hi - self.lo) / (n - 1.0))
 
-    def shift_separation(self, target_separation: float):
-        """``HjDataHandle.update_separation_distance`` (safety_filter.py:170-174)."""
-        shift = target_separation - self.separation_distance
-        if shift != 0:
-            self.values_hj -= shift           # float32 in-place, as the reference
-        self.separation_distance = target_separation
-        return shift
-
     def device_grads(self):
         """Grads padded to 4 or 8 float32 per node for 16-byte corner loads."""
         g = np.ascontiguousarray(self.grads_hj, dtype=F32).reshape(-1, self.ndim)
@@ -272,14 +264,17 @@ def load_stored_pickle(path: str) -> dict:
     return d
 
 
-def default_tables(dynamics: str, small: bool = False):
-    """(value_table, ttr_table) for a dynamics type; ``small`` shrinks the grids for tests."""
+def default_tables(dynamics: str, small: bool = False, target_separation=None):
+    """(value_table, ttr_table) for a dynamics type; ``small`` shrinks the grids for tests.
+    ``target_separation``: what HjDataHandle is built with (the scenario's
+    separation_distance_init; default the config's SEPARATION_DISTANCE)."""
     if dynamics == "double_integrator":
         shape = (31, 31, 21, 21) if small else DI_SHAPE_FULL
         st = synthetic_di_stored(shape)
-        return value_table_from_stored(st, DoubleIntegratorConfig.SEPARATION_DISTANCE), None
+        sep = DoubleIntegratorConfig.SEPARATION_DISTANCE if target_separation is None else target_separation
+        return value_table_from_stored(st, sep), None
     shape = (25, 25, 24, 7, 7) if small else AT_SHAPE_FULL
     tshape = (25, 25, 24, 7) if small else TTR_SHAPE_FULL
     st = synthetic_airtaxi_stored(shape)
-    return (value_table_from_stored(st, AirTaxiConfig.SEPARATION_DISTANCE),
-            ttr_table_from_stored(synthetic_ttr(tshape)))
+    sep = AirTaxiConfig.SEPARATION_DISTANCE if target_separation is None else target_separation
+    return (value_table_from_stored(st, sep), ttr_table_from_stored(synthetic_ttr(tshape)))

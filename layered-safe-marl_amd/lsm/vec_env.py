@@ -131,7 +131,7 @@ class GpuGraphVecEnv:
         capi.check(rc, h)
         # HJ / TTR tables (synthetic stand-ins for the absent pickles unless given)
         if a.use_safety_filter or not di:
-            vt, tt = default_tables(a.dynamics_type, small=small_tables)
+            vt, tt = default_tables(a.dynamics_type, small=small_tables, target_separation=a.initial_separation())
             value_table = value_table if value_table is not None else vt
             ttr_table = ttr_table if ttr_table is not None else tt
         self.value_table = value_table if a.use_safety_filter else None
@@ -140,7 +140,7 @@ class GpuGraphVecEnv:
             self._upload_value_table()
         if self.ttr_table is not None:
             t = self.ttr_table
-            self._set_table(self.lib.lsm_set_ttr_table, t, t.values_hj, None, extra=float(t.ttr_max))
+            self._set_table(self.lib.lsm_set_ttr_table, t, t.values_hj, None, extra=(float(t.ttr_max),))
         # outputs
         self.E = int(self.lib.lsm_num_entities(h))
         self.F = int(self.lib.lsm_node_features(h))
@@ -186,11 +186,10 @@ class GpuGraphVecEnv:
         self._pending = None
         self._cur_cache = {}
         self._last_ep = 0
-        self._sep_tracked = None
         self.closed = False
 
     # -- tables ------------------------------------------------------------------------
-    def _set_table(self, fn, t: HjTable, values, grads, extra=None):
+    def _set_table(self, fn, t: HjTable, values, grads, extra=()):
         nd = t.ndim
         lo = (C.c_double * nd)(*[float(x) for x in t.lo])
         hi = (C.c_double * nd)(*[float(x) for x in t.hi])
@@ -201,21 +200,16 @@ class GpuGraphVecEnv:
         if grads is not None:
             g = np.ascontiguousarray(grads, dtype=np.float32)
             args.append(g.ctypes.data_as(C.c_void_p))
-        if extra is not None:
-            args.append(extra)
+        args.extend(extra)
         capi.check(fn(*args), self.h)
 
     def _upload_value_table(self):
+        """HjDataHandle.__init__ (safety_filter.py:155-168): the table is read-only after this;
+        each env's own `update_separation_distance` history (safety_filter.py:170-174) is applied
+        on the device at its resets."""
         t = self.value_table
-        self._set_table(self.lib.lsm_set_value_table, t, t.values_hj, t.device_grads())
-
-    def _track_separation(self, block):
-        """HjDataHandle.update_separation_distance: values_hj -= shift (float32, in place)."""
-        if self.value_table is None:
-            return
-        sep = block["separation_distance"]
-        if self.value_table.shift_separation(sep) != 0:
-            self._upload_value_table()
+        self._set_table(self.lib.lsm_set_value_table, t, t.values_hj, t.device_grads(),
+                        extra=(float(t.separation_distance),))
 
     # -- vec-env API -------------------------------------------------------------------------
     def _stream(self):
@@ -223,7 +217,6 @@ class GpuGraphVecEnv:
 
     def reset(self, num_current_episode: int = 0):
         block = curriculum_block(self.args, num_current_episode)
-        self._track_separation(block)
         self._last_ep = num_current_episode
         cur = to_struct(block)
         capi.check(self.lib.lsm_reset(self.h, C.byref(cur), self._stream()), self.h)

@@ -17,9 +17,12 @@ Pinned by ``tests/golden/*.npz`` (recorded from the reference itself by
 ``tests/golden/make_golden.py``); see ``tests/test_oracle_golden.py``.
 
 ``integrator='rk45'`` calls scipy's ``solve_ivp(..., 'RK45')`` exactly like
-``core.py:118-131,199-210``; ``integrator='closed'`` uses the closed-form
-solution the HIP kernel uses (equal to RK45 within ~1e-15, see
-``tests/test_oracle_golden.py::test_closed_form_matches_rk45``).
+``core.py:118-131,199-210``; ``integrator='restated'`` is what the HIP kernel
+computes: for the double integrator the C restatement of that RK45 call
+(``oracle/csrc/rk45_ref.c``, bit-exact with scipy here, ``tests/test_rk45.py``),
+for airtaxi the closed form; ``integrator='closed'`` is the closed form for both
+(equal to RK45 within ~1e-15 / 1e-12, but not at the last bit, which decides ties
+at the filter's clip thresholds).
 """
 from __future__ import annotations
 
@@ -197,7 +200,11 @@ class OracleEnv:
         self.eng_ref = C.ENGAGEMENT_DISTANCE
         self.eng_ref_sep = C.ENGAGEMENT_DISTANCE_REFERENCE_SEPARATION_DISTANCE
         self.sep_target = C.SEPARATION_DISTANCE
-        self.sep_init = self.sep_target
+        # navigation_graph_safe.py:183-191: RewardBinaryConfig.SEPARATION_DISTANCE_CURRICULUM (False in
+        # config.py:81) starts the separation at 0; HjDataHandle is built at that separation
+        # (core.py:429,456) and every reset shifts this env's own values_hj (safety_filter.py:170-174)
+        self.sep_curriculum = bool(g("separation_distance_curriculum") or False)
+        self.sep_init = 0 if self.sep_curriculum else self.sep_target
         self.separation_distance = self.sep_init
         self.engagement_distance = self.eng_ref + (self.separation_distance - self.eng_ref_sep)
         self.world_engagement_distance = C.ENGAGEMENT_DISTANCE
@@ -727,7 +734,15 @@ class OracleEnv:
                     return np.array([y[3] * np.cos(y[2]), y[3] * np.sin(y[2]), a[0], a[1]])
             sol = solve_ivp(ode, [0, dt], self.s[i], method="RK45")
             self.s[i] = sol.y[:, -1]
+        elif self.integrator == "restated" and self.di:
+            # the C restatement of scipy's RK45 for this ODE (oracle/csrc/rk45_ref.c), bit-exact
+            # with solve_ivp in this image and much faster
+            y = np.ascontiguousarray(self.s[i], dtype=np.float64).copy()
+            _rk45_ref().rk45_di_ref(y.ctypes.data, float(a[0]), float(a[1]), float(dt))
+            self.s[i] = y
         else:
+            # "closed" (and "restated" for airtaxi, whose RK45 right-hand side calls numpy's SIMD
+            # cos / sin: not restatable bit-exactly; the closed form agrees to ~1e-12)
             self.s[i] = closed_form_step(self.s[i], a, dt, self.di)
         if self.di:
             spd = self.speed(i)
@@ -896,6 +911,26 @@ def closed_form_step(y, a, dt, di):
     px = y[0] + (A * cm * sc + B * sm * q)
     py = y[1] + (A * sm * sc - B * cm * q)
     return np.array([px, py, th1, v1])
+
+
+_RK45 = None
+
+
+def _rk45_ref():
+    """oracle/liboracle_ref.so (built by oracle/build_ref.py, in __graft_entry__.build())."""
+    global _RK45
+    if _RK45 is None:
+        import ctypes
+        import os
+        path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "liboracle_ref.so")
+        if not os.path.exists(path):
+            from oracle import build_ref
+            build_ref.build()
+        lib = ctypes.CDLL(path)
+        lib.rk45_di_ref.argtypes = [ctypes.c_void_p, ctypes.c_double, ctypes.c_double, ctypes.c_double]
+        lib.rk45_di_ref.restype = ctypes.c_int
+        _RK45 = lib
+    return _RK45
 
 
 class OracleVecEnv:

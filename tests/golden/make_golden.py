@@ -59,19 +59,33 @@ def pack_adj(adj_list):
 
 
 def run_case(name, args, seed, ep, steps, value_stored=None, ttr_stored=None, inject=None,
-             action_seed=0):
+             action_seed=0, runner_episodes=False, sep_curriculum=False):
+    """runner_episodes: step t passes the runner's episode counter ep + t // episode_length, as
+    GMPERunner.run does (graph_mpe_runner.py:72-103), so the worker's auto-resets
+    (env_wrappers.py:866-871) move through the curriculum. sep_curriculum: the reference's
+    RewardBinaryConfig.SEPARATION_DISTANCE_CURRICULUM (config.py:81) set while the env is made
+    (make_world reads it, navigation_graph_safe.py:183-191)."""
     work = tempfile.mkdtemp(prefix="lsm_ref_")
     di = args.dynamics_type == "double_integrator"
     if value_stored is not None or ttr_stored is not None:
         ref_harness.write_data_files(work, di_table=value_stored if di else None,
                                      at_table=None if di else value_stored, ttr_table=ttr_stored)
-    env = ref_harness.make_reference_env(args, work, seed)
+    if sep_curriculum:
+        from multiagent.config import RewardBinaryConfig
+        old = RewardBinaryConfig.SEPARATION_DISTANCE_CURRICULUM
+        RewardBinaryConfig.SEPARATION_DISTANCE_CURRICULUM = True
+        try:
+            env = ref_harness.make_reference_env(args, work, seed)
+        finally:
+            RewardBinaryConfig.SEPARATION_DISTANCE_CURRICULUM = old
+    else:
+        env = ref_harness.make_reference_env(args, work, seed)
     scen = env.reward_callback.__self__
     world = env.world
     N = args.num_agents
     rng = np.random.default_rng(action_seed)
     rec = {k: [] for k in ("act", "state", "reached", "done", "dones", "rew", "obs", "adj_bits",
-                           "minrel", "sfilt", "decon", "edges_n", "info_num", "ptime")}
+                           "minrel", "sfilt", "decon", "edges_n", "info_num", "ptime", "step_ep", "hj_sep")}
     full = {}
     resets = []
 
@@ -99,6 +113,7 @@ def run_case(name, args, seed, ep, steps, value_stored=None, ttr_stored=None, in
         st = np.array([a.state.values for a in world.agents])
         a_idx = policy(st, goals(), rng, di)
         onehot = ref_harness.one_hot_actions(a_idx)
+        ep_t = ep + t // args.episode_length if runner_episodes else ep
         res = ref_harness.run_in(work, env.step, list(onehot))
         obs, aid, node, adj, rew, done_n, info = res
         edges = np.array(world.edge_list)
@@ -116,13 +131,16 @@ def run_case(name, args, seed, ep, steps, value_stored=None, ttr_stored=None, in
         rec["edges_n"].append(edges.shape[1])
         rec["info_num"].append(np.array([[inf[k] for k in INFOKEYS] for inf in info], dtype=np.float64))
         rec["ptime"].append(np.array([a.state.p_dist for a in world.agents]))
+        rec["step_ep"].append(ep_t)
+        hj = world.hj_data_handle
+        rec["hj_sep"].append(float(hj.separation_distance) if hj is not None else np.nan)
         changed = t > 0 and not np.array_equal(rec["done"][-1], rec["done"][-2])
         if t in FULL_STEPS or t % 50 == 0 or changed:
             full["t%03d_node" % t] = np.array(node, dtype=np.float32)
             full["t%03d_adj" % t] = np.array(adj, dtype=np.float32)
             full["t%03d_edges" % t] = edges
         if np.all(done_n):
-            r = ref_harness.run_in(work, env.reset, ep)
+            r = ref_harness.run_in(work, env.reset, ep_t)
             obs, aid, node, adj, epinfo = r
             resets.append((t + 1, [epinfo[k] for k in EPKEYS]))
             full["t%03d_reset_obs" % t] = np.array(obs)
@@ -136,9 +154,13 @@ def run_case(name, args, seed, ep, steps, value_stored=None, ttr_stored=None, in
     out["resets_t"] = np.array([r[0] for r in resets])
     out["resets_info"] = np.array([r[1] for r in resets], dtype=np.float64)
     meta = dict(vars(args)); meta.update(name=name, env_seed=seed, ep=ep, steps=steps)
+    if sep_curriculum:
+        meta["separation_distance_curriculum"] = True
     out["meta"] = np.array(repr(meta))
     path = os.path.join(HERE, name + ".npz")
     np.savez_compressed(path, **out)
+    if runner_episodes:
+        print("  separations at the steps:", sorted(set(float(x) for x in out["hj_sep"])))
     print("wrote", path, os.path.getsize(path) // 1024, "KB;",
           "done agents at end:", int(out["done"][-1].sum()), "resets:", len(resets) - 1,
           "filtered steps:", int(out["sfilt"].sum()))
@@ -165,10 +187,32 @@ def inject_goal_arrival(world, scen):
     world.calculate_distances()
 
 
-def main():
+def main(only=None):
     if not ref_harness.reference_available():
         raise SystemExit("reference not available here")
     A = ref_harness.default_args
+    di_small = hj_tables.synthetic_di_stored((31, 31, 21, 21))
+    at_small = hj_tables.synthetic_airtaxi_stored((25, 25, 24, 7, 7))
+    ttr_small = hj_tables.synthetic_ttr((25, 25, 24, 7))
+    # the runner's call pattern with the separation curriculum: episode index advancing across
+    # auto-resets through the stair levels 0.25 -> 0.5 -> 0.75 -> 1 (num_total_episode = 10),
+    # each env's HJ table shifted at its own resets (safety_filter.py:170-174)
+    sepcur = [
+        lambda: run_case("di_n4_sepcur", A(num_agents=4, num_env_steps=40 * 10, episode_length=40,
+                                           use_safety_filter=True),
+                         seed=21, ep=3, steps=260, value_stored=di_small, action_seed=8,
+                         runner_episodes=True, sep_curriculum=True),
+        lambda: run_case("at_n3_sepcur", A(num_agents=3, num_env_steps=30 * 10, dynamics_type="airtaxi",
+                                           world_size=6, episode_length=30, use_safety_filter=True),
+                         seed=23, ep=3, steps=200, value_stored=at_small, ttr_stored=ttr_small,
+                         action_seed=9, runner_episodes=True, sep_curriculum=True),
+    ]
+    if only == "sepcur":
+        for f in sepcur:
+            f()
+        return
+    for f in sepcur:
+        f()
     di_small = hj_tables.synthetic_di_stored((31, 31, 21, 21))
     at_small = hj_tables.synthetic_airtaxi_stored((25, 25, 24, 7, 7))
     ttr_small = hj_tables.synthetic_ttr((25, 25, 24, 7))
@@ -189,4 +233,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1] if len(sys.argv) > 1 else None)

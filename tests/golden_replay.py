@@ -41,10 +41,19 @@ def tables_for(meta):
     if meta["use_safety_filter"]:
         st = hj_tables.synthetic_di_stored((31, 31, 21, 21)) if di else \
             hj_tables.synthetic_airtaxi_stored((25, 25, 24, 7, 7))
-        vt = hj_tables.value_table_from_stored(st, st["separation_distance"])
+        # HjDataHandle is built at the scenario's initial separation: 0 with the separation
+        # curriculum (navigation_graph_safe.py:183-191), else the config's
+        sep0 = 0 if meta.get("separation_distance_curriculum") else st["separation_distance"]
+        vt = hj_tables.value_table_from_stored(st, sep0)
     if not di:
         tt = hj_tables.ttr_table_from_stored(hj_tables.synthetic_ttr((25, 25, 24, 7)))
     return vt, tt
+
+
+def step_ep(z, meta, t):
+    """The episode index the fixture passed with step t (the runner's counter when recorded with
+    runner_episodes, else the fixed ep); also the ep of an auto-reset after step t."""
+    return int(z["step_ep"][t]) if "step_ep" in z.files and len(z["step_ep"]) else int(meta["ep"])
 
 
 def table_dict(t):

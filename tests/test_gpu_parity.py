@@ -5,7 +5,7 @@ pattern / done masks bit-exact; fp32 outputs within 1e-5; float64 states within 
 import numpy as np
 import pytest
 
-from golden_replay import EPKEYS, INFOKEYS, adj_bits, fixture_names, load, table_dict, tables_for
+from golden_replay import EPKEYS, INFOKEYS, adj_bits, fixture_names, load, step_ep, table_dict, tables_for
 
 pytestmark = pytest.mark.gpu
 
@@ -54,7 +54,7 @@ def test_gpu_matches_reference_golden(name, kernel, monkeypatch):
     c_rg = _info_col("reached_goal")
     for t in range(meta["steps"]):
         ctx = "%s step %d" % (name, t)
-        obs, aid, node, adj, rew, dones, infos = env.step(z["act"][t][None], meta["ep"])
+        obs, aid, node, adj, rew, dones, infos = env.step(z["act"][t][None], step_ep(z, meta, t))
         info = env.t_info.cpu().numpy()[0]
         reset = bool(env.t_reset.cpu().numpy()[0])
         np.testing.assert_array_equal(dones[0], z["dones"][t], err_msg=ctx)
@@ -97,7 +97,7 @@ def _oracle_for(meta, seed, n_envs, env_offset=0):
     from oracle.lsm_oracle import OracleVecEnv
     vt, tt = tables_for(meta)
     return OracleVecEnv(meta, n_envs, seed=seed, value_table=table_dict(vt), ttr_table=table_dict(tt),
-                        integrator="closed", seed_offset=env_offset)
+                        integrator="restated", seed_offset=env_offset)
 
 
 CASES = [
@@ -359,3 +359,113 @@ def test_gpu_action_encodings_and_dummy_semantics():
             assert g[5].all()                    # past the end: every agent done, no reset
     assert not gpu.t_reset.cpu().numpy().any()
     gpu.close()
+
+
+def _goal_policy(envs, rng, eps=0.1):
+    """Goal-seeking discrete actions from the oracle envs' states (make_golden.py's policy)."""
+    out = []
+    for e in envs:
+        idx = np.zeros(e.N, dtype=np.int64)
+        for i in range(e.N):
+            if rng.random() < eps:
+                idx[i] = rng.integers(0, 25)
+                continue
+            g, s = e.lm_pos[e.goal_index(i)], e.s[i]
+            acc = 1.2 * (g - s[:2]) - 1.5 * s[2:]
+            q = np.clip(np.round(acc / 0.25), -2, 2).astype(int) + 2
+            idx[i] = q[0] * 5 + q[1]
+        out.append(idx)
+    return np.array(out)
+
+
+def _arrive_all(e):
+    """Every agent of oracle env e placed on its last goal at the goal's speed and heading with
+    reached_goal = L - 1 (make_golden.py's inject_goal_arrival for all agents): with zero
+    acceleration the next step reaches every final goal, so the env is all-done early."""
+    L, N = e.L, e.N
+    st = e.s.copy()
+    for i in range(N):
+        g = (L - 1) * N + i
+        sp, h = e.lm_speed[g], e.lm_heading[g]
+        st[i] = [e.lm_pos[g][0], e.lm_pos[g][1], sp * np.cos(h), sp * np.sin(h)]
+    return st, np.full(N, L - 1, dtype=np.int32)
+
+
+@pytest.mark.parametrize("kernel", ["wave", "block"])
+def test_gpu_runner_call_pattern_separation_curriculum(kernel, monkeypatch):
+    """GMPERunner's real call pattern (graph_mpe_runner.py:72-103): step(actions, episode) with the
+    episode index advancing every episode_length steps, the worker auto-resetting with it
+    (env_wrappers.py:866-871). With SEPARATION_DISTANCE_CURRICULUM each reset shifts that env's own
+    HJ table (safety_filter.py:170-174 via navigation_graph_safe.py:349-364); envs driven all-done
+    mid-episode reset at the newer stair level while the others keep the older one, so envs hold
+    different tables at once. 16 envs vs the oracle, every step."""
+    if kernel == "block":
+        monkeypatch.setenv("LSM_KERNEL", "block")
+    epl, ep0, n_envs, N = 60, 3, 16, 3
+    meta = dict(dynamics_type="double_integrator", num_agents=N, num_landmarks=2, world_size=4,
+                episode_length=epl, num_env_steps=epl * 10, n_rollout_threads=1, use_safety_filter=True,
+                use_masking=True, num_internal_step=1, seed=9, env_seed=9, separation_distance_curriculum=True)
+    env = _gpu_env(meta, n_envs=n_envs, seed=9)
+    ora = _oracle_for(meta, 9, n_envs)
+    g, o = env.reset(ep0), ora.reset(ep0)
+    np.testing.assert_allclose(g[0], o[0], rtol=0, atol=F32_ATOL)
+    rng = np.random.default_rng(17)
+    early = {epl + 20: (0, 5, 11), 2 * epl + 7: (0, 3), 3 * epl + 30: (5, 9, 14), 3 * epl + 31: (5,)}
+    c_sf = _info_col("Safety filtered")
+    split_seen = early_resets = 0
+    for t in range(5 * epl):
+        ep = ep0 + t // epl
+        a = _goal_policy(ora.envs, rng)
+        for k in early.get(t - 1, ()):
+            a[k] = 12                                       # zero acceleration after the arrival
+        g = env.step(a, ep)
+        o = ora.step(a, ep)
+        ctx = "step %d ep %d" % (t, ep)
+        np.testing.assert_array_equal(g[5], o[5], err_msg=ctx)
+        np.testing.assert_array_equal(g[3] != 0, o[3] != 0, err_msg=ctx)
+        np.testing.assert_allclose(g[0], o[0], rtol=0, atol=F32_ATOL, err_msg=ctx)
+        np.testing.assert_allclose(g[2], o[2], rtol=0, atol=F32_ATOL, err_msg=ctx)
+        np.testing.assert_allclose(g[3], o[3], rtol=0, atol=F32_ATOL, err_msg=ctx)
+        np.testing.assert_allclose(g[4], o[4], rtol=1e-6, atol=1e-5, err_msg=ctx)
+        st = env.state().cpu().numpy()
+        info = env.t_info.cpu().numpy()
+        for k, e in enumerate(ora.envs):
+            np.testing.assert_allclose(st[k], e.s, rtol=0, atol=STATE_ATOL, err_msg=ctx)
+            np.testing.assert_array_equal(info[k, :, c_sf].astype(bool),
+                                          [bool(x["Safety filtered"]) for x in o[6][k][:N]], err_msg=ctx)
+        reset = env.t_reset.cpu().numpy()
+        if (t + 1) % epl:
+            early_resets += int(reset.sum())
+        split_seen += len({e.hj_sep for e in ora.envs}) > 1
+        for k in early.get(t, ()):                          # drive env k all-done at the next step
+            s, r = _arrive_all(ora.envs[k])
+            env.set_agent_state(k, s, r)
+            e = ora.envs[k]
+            e.s[:] = s
+            e.reached_goal[:] = r
+            e.calculate_distances()
+    assert early_resets >= 8, early_resets
+    assert split_seen > 0
+    env.close()
+
+
+@pytest.mark.gpu
+def test_gpu_separation_chain_bound():
+    """The per-env shift chain holds at most 8 separation changes per table upload: a 9th change of
+    the separation across calls is refused with an error (nothing launched), and re-uploading the
+    table starts afresh."""
+    from lsm import capi
+    meta = dict(dynamics_type="double_integrator", num_agents=3, num_landmarks=2, world_size=4,
+                episode_length=5, num_env_steps=5 * 20, n_rollout_threads=1, use_safety_filter=True,
+                use_masking=True, num_internal_step=1, seed=1, env_seed=1, separation_distance_curriculum=True)
+    env = _gpu_env(meta, n_envs=2, seed=1)
+    # stair levels of ep = 0, 4, 8, 12, 16 (0, .25, .5, .75, 1); alternate up and down
+    seq = [4, 8, 12, 16, 12, 8, 4, 8]
+    env.reset(0)
+    for ep in seq:
+        env.reset(ep)
+    with pytest.raises(capi.LsmError, match="separation-distance changes"):
+        env.reset(12)
+    env._upload_value_table()
+    env.reset(12)
+    env.close()

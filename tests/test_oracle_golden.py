@@ -11,7 +11,7 @@ episode summaries returned at each reset.
 import numpy as np
 import pytest
 
-from golden_replay import EPKEYS, INFOKEYS, adj_bits, fixture_names, load, table_dict, tables_for
+from golden_replay import EPKEYS, INFOKEYS, adj_bits, fixture_names, load, step_ep, table_dict, tables_for
 from oracle.hj_grid import Grid
 from oracle.lsm_oracle import OracleEnv, closed_form_step
 
@@ -27,9 +27,15 @@ def _replay(name, integrator="rk45"):
     return z, meta, env, out
 
 
+@pytest.mark.parametrize("integrator", ["rk45", "restated"])
 @pytest.mark.parametrize("name", NAMES)
-def test_oracle_matches_reference(name):
-    z, meta, env, (obs, aid, node, adj, info) = _replay(name)
+def test_oracle_matches_reference(name, integrator):
+    """integrator='rk45' is the reference's own solve_ivp call; 'restated' is what the kernel
+    computes (the C restatement of that call for the double integrator, the closed form for
+    airtaxi): both must reproduce the double-integrator fixtures bit for bit."""
+    if integrator == "restated" and not name.startswith("di_"):
+        pytest.skip("airtaxi: the kernel's closed form agrees with RK45 to ~1e-12, not bit for bit")
+    z, meta, env, (obs, aid, node, adj, info) = _replay(name, integrator)
     np.testing.assert_array_equal(np.array(obs), z["reset0_obs"])
     np.testing.assert_array_equal(np.array(node, dtype=np.float32), z["reset0_node"])
     np.testing.assert_array_equal(np.array(adj, dtype=np.float32), z["reset0_adj"])
@@ -59,13 +65,15 @@ def test_oracle_matches_reference(name):
             np.array([[inf[k] for k in INFOKEYS] for inf in infos], dtype=np.float64), z["info_num"][t],
             err_msg=ctx)
         np.testing.assert_array_equal(env.p_dist, z["ptime"][t], err_msg=ctx)
+        if "hj_sep" in z.files and env.use_safety_filter:
+            assert env.hj_sep == z["hj_sep"][t], ctx
         key = "t%03d_node" % t
         if key in z.files:
             np.testing.assert_array_equal(np.array(node, dtype=np.float32), z[key], err_msg=ctx)
             np.testing.assert_array_equal(np.array(adj, dtype=np.float32), z["t%03d_adj" % t], err_msg=ctx)
             np.testing.assert_array_equal(env.edge_list, z["t%03d_edges" % t], err_msg=ctx)
         if np.all(dones):
-            obs, aid, node, adj, info = env.reset(meta["ep"])
+            obs, aid, node, adj, info = env.reset(step_ep(z, meta, t))
             assert z["resets_t"][n_reset] == t + 1
             np.testing.assert_array_equal([info[k] for k in EPKEYS], z["resets_info"][n_reset], err_msg=ctx)
             np.testing.assert_array_equal(env.s, z["t%03d_reset_state" % t], err_msg=ctx)
