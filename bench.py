@@ -10,6 +10,11 @@ envs sharded by global index (weak scaling), RCCL all_reduce of the episode
 summary at each episode boundary, max-over-ranks timing.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4|5]
+
+--gpus N > 1 starts N rank processes itself (or runs under torchrun, WORLD_SIZE = N). The timed
+window always straddles an episode boundary (auto-reset launch + RCCL episode summary): the
+untimed steps before it are at least --warmup, padded to that phase ("warmup" in the line is the
+count actually run).
 """
 from __future__ import annotations
 
@@ -145,6 +150,82 @@ def bench_edges(env, dev, reps=50):
             "L2/MALL hits"}
 
 
+def cpu_share():
+    """(cores this job may use, host cores): the affinity set, capped by a cgroup CPU quota if
+    one is set (a GPU box lends each GPU a share of a larger host)."""
+    host = len(os.sched_getaffinity(0))
+    n = host
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            n = max(1, min(n, int(int(q) // int(period))))
+    except Exception:
+        pass
+    return n, host
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch(a):
+    """--gpus N > 1 without a launcher: start N fresh rank processes (one per GPU) before this
+    process touches any GPU, each with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, and exit with
+    the worst return code. Rank 0 prints the JSON line."""
+    import subprocess
+    port = _free_port()
+    procs = []
+    for r in range(a.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(a.gpus), LOCAL_WORLD_SIZE=str(a.gpus),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc != 0]
+    return bad[0] if bad else 0
+
+
+def timed_window(warmup, steps, epl):
+    """Untimed steps before the timed window: at least `warmup`, and as many more as put an
+    episode boundary (the auto-reset launch and the episode-summary collective) in the middle of
+    the window, whatever --steps is."""
+    return warmup + (epl - (warmup + steps // 2) % epl) % epl
+
+
+def dry_run(a, rank, world):
+    """--dry-run: the multi-rank plumbing without a GPU (gloo): ranks, env offsets, the
+    episode-summary collective and the max-over-ranks timing reduction."""
+    import torch
+    import torch.distributed as dist
+    from lsm.dist import global_episode_summary
+    c = CONFIGS[a.config]
+    n_envs = a.envs or c["envs"]
+    if world > 1:
+        dist.init_process_group("gloo")
+        assert dist.get_world_size() == a.gpus, (dist.get_world_size(), a.gpus)
+    ep = torch.arange(n_envs * 8, dtype=torch.float64).reshape(n_envs, 8) + rank * n_envs * 8
+    summ = global_episode_summary(ep)
+    info = torch.tensor([rank, rank * n_envs, n_envs, time.perf_counter()], dtype=torch.float64)
+    if world > 1:
+        allv = [torch.zeros_like(info) for _ in range(world)]
+        dist.all_gather(allv, info)
+        ms = torch.tensor([1.0 + rank], dtype=torch.float64)
+        dist.all_reduce(ms, op=dist.ReduceOp.MAX)
+    else:
+        allv, ms = [info], torch.tensor([1.0])
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": world, "world_size": world,
+                          "ranks": [{"rank": int(v[0]), "env_offset": int(v[1]), "envs": int(v[2])} for v in allv],
+                          "max_over_ranks": float(ms[0]), "episode_summary": summ,
+                          "untimed_steps": timed_window(a.warmup, a.steps, c["episode_length"])}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -160,10 +241,19 @@ def main():
     ap.add_argument("--edges", action="store_true",
                     help="also time GNNBase.process_adj (lsm_edges.hip) on the final adjacency and add an "
                          "'edges' object to the JSON line (SURVEY 8(f) row 2; not part of the step)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="no GPU: check the rank launch, env offsets and collectives with gloo")
     a = ap.parse_args()
 
     from lsm.dist import rank_info, global_episode_summary
+    launched = "WORLD_SIZE" in os.environ
+    if not launched and a.gpus > 1:
+        sys.exit(launch(a))
     rank, world, local_rank = rank_info()
+    if world != a.gpus:
+        raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%d (one rank per GPU)" % (a.gpus, world))
+    if a.dry_run:
+        return dry_run(a, rank, world)
     c = CONFIGS[a.config]
     n_envs = a.envs or c["envs"]
     args = make_args(c)
@@ -174,15 +264,20 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        cores = a.cpu_cores or min(16, len(os.sched_getaffinity(0)))
+        share, host = cpu_share()
+        cores = a.cpu_cores or share
         epw, csteps = c.get("cpu_sample", (4, 500))
         cpu = cpu_baseline(args, table_dict(vt), table_dict(tt), ep, cores, envs_per_worker=epw, steps=csteps)
+        cpu["host_cores"] = host
+        cpu["cpu_share"] = share
 
     import torch
     import torch.distributed as dist
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         dist.init_process_group("nccl")
+        if dist.get_world_size() != a.gpus:
+            raise SystemExit("RCCL world size %d != --gpus %d" % (dist.get_world_size(), a.gpus))
     dev = torch.device("cuda:%d" % local_rank)
     torch.cuda.set_device(dev)
     from lsm.vec_env import GpuGraphVecEnv
@@ -190,12 +285,13 @@ def main():
     env = GpuGraphVecEnv(args, num_envs=n_envs, device=dev, value_table=vt, ttr_table=tt,
                          env_offset=rank * n_envs, return_numpy=False, build_infos=False, adj_layout=layout)
     N = c["num_agents"]
+    epl = c["episode_length"]
+    pre = timed_window(a.warmup, a.steps, epl)
     gen = torch.Generator(device=dev).manual_seed(1234 + rank)
     # Synthetic policy: every step's discrete actions drawn up front, resident in HBM before the
     # timed region (the policy is outside the path; one env-step = one rollout_kernel launch).
-    acts_all = torch.randint(0, 25, (a.warmup + a.steps, n_envs, N), generator=gen, device=dev,
+    acts_all = torch.randint(0, 25, (pre + a.steps, n_envs, N), generator=gen, device=dev,
                              dtype=torch.int32)
-    epl = c["episode_length"]
     buf = None
     if a.buffer:
         from lsm.buffer import DeviceGraphBuffer
@@ -216,7 +312,7 @@ def main():
             global_episode_summary(env.t_epinfo)
 
     global_episode_summary(env.t_epinfo)   # load the reduction kernels before any timed call
-    for t in range(a.warmup):
+    for t in range(pre):
         one_step(t)
     # Kernel time: HIP events on the launch stream bracketing the whole timed region (per-launch
     # event pairs would add their own GPU-side markers between back-to-back launches).
@@ -228,7 +324,7 @@ def main():
     t0 = time.perf_counter()
     ev0.record()
     for t in range(a.steps):
-        one_step(a.warmup + t)
+        one_step(pre + t)
     ev1.record()
     torch.cuda.synchronize()
     if world > 1:
@@ -236,10 +332,14 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     kern_ms = ev0.elapsed_time(ev1) / a.steps   # includes the inter-launch gaps (conservative)
+    per_rank = [elapsed * 1e3 / a.steps]
     if world > 1:
-        tt_ = torch.tensor([elapsed, kern_ms], device=dev, dtype=torch.float64)
-        dist.all_reduce(tt_, op=dist.ReduceOp.MAX)
-        elapsed, kern_ms = tt_.tolist()
+        mine = torch.tensor([elapsed, kern_ms], device=dev, dtype=torch.float64)
+        allt = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(allt, mine)
+        per_rank = [float(x[0]) * 1e3 / a.steps for x in allt]
+        elapsed = max(float(x[0]) for x in allt)
+        kern_ms = max(float(x[1]) for x in allt)
     total_agent_steps = world * n_envs * N * a.steps
     value = total_agent_steps / elapsed
     from lsm.perf_model import step_bytes
@@ -247,14 +347,17 @@ def main():
     bytes_launch = sb["hbm_bytes"] * n_envs
     achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
     traffic = load_traffic(a.config, n_envs)
+    resets = int((pre + a.steps) // epl - pre // epl)
     if rank == 0:
         line = {
             "metric": METRIC, "value": value, "unit": "agent-steps/s", "n_gpus": world, "steps": a.steps,
-            "warmup": a.warmup, "ms_per_step": elapsed * 1e3 / a.steps, "higher_is_better": True,
+            "warmup": pre, "warmup_requested": a.warmup, "ms_per_step": elapsed * 1e3 / a.steps,
+            "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
             "config": {"workload": c["workload"], "num_agents": N, "envs_per_gpu": n_envs,
                        "total_envs": world * n_envs, "dynamics": c["dynamics_type"],
                        "safety_filter": c["use_safety_filter"], "episode_length": epl,
+                       "episode_boundaries_timed": resets,
                        "output_layout": ("reference (per-ego node_obs/adj, fp32)" if layout == "reference" else
                                          "per-ego node_obs fp32; compact adjacency (E x E fp32 + per-ego "
                                          "u64 disconnect masks, lossless)"),
@@ -262,12 +365,14 @@ def main():
                        "parallelism": "env-sharded dp%d" % world,
                        "handoff": ("DeviceGraphBuffer rows (ring-bound outputs + insert kernel)" if a.buffer
                                    else "env output tensors")},
+            "ranks": {"rccl_world_size": (dist.get_world_size() if world > 1 else 1), "ms_per_step": per_rank},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
                          "frac": achieved / PEAK_HBM_GBPS, "traffic": traffic, "traffic_unit": "HBM bytes/launch (rocprofv3 PMC)",
                          "kernel": "%s<%d>" % ("rollout_block_kernel" if sb["block"] else "rollout_kernel",
                                                0 if c["dynamics_type"] == "double_integrator" else 1),
                          "kernel_ms": kern_ms, "algorithmic_bytes_per_launch": bytes_launch,
-                         "gather_bytes_per_launch": sb["gather_bytes"] * n_envs},
+                         "gather_bytes_per_launch": sb["gather_bytes"] * n_envs,
+                         "bytes_model": "lsm/perf_model.py: record + outputs + HJ gathers (SURVEY 8(d))"},
             "cpu_baseline": cpu,
         }
         if a.edges:

@@ -168,6 +168,11 @@ int lsm_bind_output_ring(lsm_env* env, int32_t slot, void* base, size_t stride_b
                          int32_t index_offset);
 int lsm_select_ring(lsm_env* env, int32_t index);
 
+/* 1 if a launch since the last call saw an index action outside [0, 25) (it was clamped to keep
+ * the launch in bounds; the reference's one-hot decode, environment.py:386-410, has no such
+ * input), else 0; -1 on error. Synchronises `hip_stream` and clears the flag. */
+int32_t lsm_action_errors(lsm_env* env, void* hip_stream);
+
 /* Shape helpers. */
 int32_t lsm_num_entities(const lsm_env* env);   /* E = N * (1 + L) */
 int32_t lsm_node_features(const lsm_env* env);  /* F */

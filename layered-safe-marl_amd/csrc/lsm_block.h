@@ -239,6 +239,7 @@ __global__ __launch_bounds__(BT) void rollout_block_kernel(const KParams* __rest
 
   // ---- 2. decode actions ----------------------------------------------------------------
   if (tid < N) {
+    if (ai < 0 || ai > 24) *gptr(P.action_err) = 1;   // lsm_action_errors() reports it
     const int a = ai < 0 ? 0 : (ai > 24 ? 24 : ai);
     const int xi = a / 5, yi = a - xi * 5;
     S.raw[tid] = P.act0[xi];

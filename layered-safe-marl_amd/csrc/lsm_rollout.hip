@@ -153,6 +153,7 @@ struct KParams {
   int diag;                       // diagnostic builds: bit 0 skip adj/node stores, bit 1 skip filter (LSM_DIAG)
   uint32_t lds_env_bytes;         // LDS bytes per env (envs per wave > 1: consecutive blocks)
   const uint16_t* pairs;          // strict upper-triangle entity pairs (a | b << 8)
+  int32_t* action_err;            // set to 1 by a launch that saw an action index outside [0, 25)
   TableDev val, ttr;
   StateDev s;
   OutDev o;
@@ -2024,6 +2025,9 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams* __restrict__
 
   // ---- 2. decode actions ----------------------------------------------------------
   if (lane < N) {
+    // an index outside Discrete(25) is an error of the caller (the reference's one-hot decode has
+    // no such input): flag it for lsm_action_errors(), and keep the launch in bounds
+    if (ai < 0 || ai > 24) *gptr(P.action_err) = 1;
     int a = ai < 0 ? 0 : (ai > 24 ? 24 : ai);
     const int xi = a / 5, yi = a - xi * 5;
     S.raw[lane] = P.act0[xi];
@@ -2220,6 +2224,7 @@ struct lsm_env {
   bool tables_ok;
   int device;
   KParams* dparams;   // device copy of the per-handle constants (re-uploaded when dirty)
+  int32_t* action_err;   // device flag: an action index outside [0, 25) since the last check
   bool params_dirty;
   // ring-bound output slots (lsm_bind_output_ring): ring index i writes slot s at
   // ring_base[s] + (i + ring_off[s]) * ring_stride[s] when that lands in [0, ring_count[s]),
@@ -2337,6 +2342,7 @@ static void fill_params(const lsm_env* e, KParams& P) {
   if (const char* v = getenv("LSM_DIAG")) P.diag = atoi(v);
 #endif
   P.pairs = e->pairs;
+  P.action_err = e->action_err;
 }
 
 extern "C" {
@@ -2426,7 +2432,9 @@ int lsm_create(const lsm_config* cfg, lsm_env** out) {
   r |= dalloc(e, &e->dparams, 1);
   r |= dalloc(e, &e->s.mt, n * MT_WORDS);
   r |= dalloc(e, &e->pairs, (size_t)e->E * (e->E - 1) / 2 + 1);
+  r |= dalloc(e, &e->action_err, 1);
   if (r) return 1;
+  HIPCHK(e, hipMemset(e->action_err, 0, sizeof(int32_t)));
   {
     // agent-agent pairs first (the only ones needing the float64 blocks), then
     // agent-landmark, then landmark-landmark: the agent block stays in the first lane pass
@@ -2826,6 +2834,15 @@ int lsm_step(lsm_env* e, const void* actions, int32_t kind, const lsm_curriculum
   L.actions = actions;
   L.emit_edges = e->cfg.emit_edges && e->out_ptr[LSM_OUT_EDGES] != nullptr;
   return launch(e, L, (hipStream_t)stream);
+}
+
+int32_t lsm_action_errors(lsm_env* e, void* stream) {
+  if (!e) return -1;
+  int32_t v = 0;
+  if (hipStreamSynchronize((hipStream_t)stream) != hipSuccess) return -1;
+  if (hipMemcpy(&v, e->action_err, sizeof v, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  if (v && hipMemset(e->action_err, 0, sizeof(int32_t)) != hipSuccess) return -1;
+  return v;
 }
 
 int lsm_host_rk45_di(const double* y0, double a0, double a1, double dt, double* y_out) {

@@ -27,6 +27,10 @@ class BufferError(RuntimeError):
 class DeviceGraphBuffer:
     def __init__(self, env, episode_length=None, use_centralized_V: bool = True):
         import torch
+        if env.return_numpy:
+            # ring-bound outputs are never written to the env's own tensors: host copies of them
+            # would be stale and cost a sync per step
+            raise BufferError("DeviceGraphBuffer needs an env built with return_numpy=False")
         self.env = env
         self.lib = capi.load_library()
         self.T = int(episode_length or env.args.episode_length)

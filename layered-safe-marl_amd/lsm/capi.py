@@ -30,7 +30,7 @@ EXPORTED = ("lsm_create", "lsm_destroy", "lsm_last_error", "lsm_set_value_table"
             "lsm_node_features", "lsm_obs_dim", "lsm_host_mt_uniforms", "lsm_host_scenario",
             "lsm_set_agent_state", "lsm_edges_workspace_bytes", "lsm_edges_count", "lsm_edges_emit",
             "lsm_edges_last_error", "lsm_bind_output_ring", "lsm_select_ring", "lsm_buffer_insert",
-            "lsm_buffer_last_error", "lsm_host_rk45_di", "lsm_host_glibc_pow")
+            "lsm_buffer_last_error", "lsm_host_rk45_di", "lsm_host_glibc_pow", "lsm_action_errors")
 
 
 class LsmConfig(C.Structure):
@@ -91,6 +91,7 @@ def load_library(path: str = LIB_PATH):
         "lsm_buffer_last_error": (C.c_char_p, []),
         "lsm_host_rk45_di": (I32, [P, D, D, D, P]),
         "lsm_host_glibc_pow": (D, [D, D]),
+        "lsm_action_errors": (I32, [P, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

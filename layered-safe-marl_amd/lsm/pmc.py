@@ -53,11 +53,24 @@ def kernel_stats(d):
     return out
 
 
+def launch_durations(d, kernel=KERNEL):
+    """Per-dispatch durations (us) of `kernel` in dispatch order (kernel_trace.csv)."""
+    rows = []
+    for r in _rows(d, "kernel_trace.csv"):
+        if kernel in r.get("Kernel_Name", ""):
+            rows.append((int(r.get("Dispatch_Id") or 0),
+                         (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3))
+    return [us for _, us in sorted(rows)]
+
+
 def main():
     ap = argparse.ArgumentParser()
     sub = ap.add_subparsers(dest="cmd", required=True)
     s = sub.add_parser("stats")
     s.add_argument("dir")
+    ln = sub.add_parser("launches")
+    ln.add_argument("dir")
+    ln.add_argument("--kernel", default=KERNEL)
     t = sub.add_parser("traffic")
     t.add_argument("fetch_dir")
     t.add_argument("write_dir")
@@ -75,6 +88,15 @@ def main():
             for n in names:
                 v, k = counter_per_launch(d, n, a.kernel)
                 print("%-24s %16.1f  (mean of %d launches)" % (n, v, k))
+        return
+    if a.cmd == "launches":
+        us = launch_durations(a.dir, a.kernel)
+        srt = sorted(us)
+        q = lambda f: srt[min(len(srt) - 1, int(f * len(srt)))]
+        print(json.dumps({"kernel": a.kernel, "launches": len(us), "mean_us": statistics.fmean(us),
+                          "p50_us": q(0.5), "p90_us": q(0.9), "max_us": srt[-1],
+                          "slowest": [(i, round(v, 2)) for i, v in sorted(enumerate(us), key=lambda x: -x[1])[:4]],
+                          "note": "the slowest launches are the auto-reset steps (MT19937 scenario replay)"}))
         return
     if a.cmd == "stats":
         for r in kernel_stats(a.dir):

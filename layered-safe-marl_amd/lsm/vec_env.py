@@ -235,7 +235,10 @@ class GpuGraphVecEnv:
         if isinstance(actions, torch.Tensor):
             t = actions.to(self.device)
         else:
-            t = torch.as_tensor(np.asarray(actions), device=self.device)
+            host = np.asarray(actions)
+            if host.ndim == 2 and host.size and (host.min() < 0 or host.max() > 24):
+                raise ValueError("action indices must be in [0, 25) (Discrete(25))")
+            t = torch.as_tensor(host, device=self.device)
         if t.dim() == 2:
             return t.to(torch.int32).contiguous(), capi.LSM_ACTIONS_INDEX_I32
         if t.dim() == 3 and t.shape[-1] == 25:
@@ -265,6 +268,7 @@ class GpuGraphVecEnv:
             out = (self.t_obs, self.agent_id, self.t_node, self.t_adj, self.t_rew, self.t_done,
                    (self.t_info, self.t_reset, self.t_epinfo))
             return out + (0,) if not self.auto_reset else out
+        self.check_actions()   # the host copies below synchronise anyway
         obs = self.t_obs.cpu().numpy()
         node = self.t_node.cpu().numpy()
         adj = self.reference_adj().cpu().numpy()
@@ -275,6 +279,15 @@ class GpuGraphVecEnv:
         if self.auto_reset:
             return obs, aid, node, adj, rew, dones, infos
         return obs, aid, node, adj, rew, dones, infos, 0
+
+    def check_actions(self):
+        """Raise if a step since the last check got an index action outside [0, 25) from a device
+        tensor (the kernel clamps it to stay in bounds and flags it). Synchronises."""
+        v = self.lib.lsm_action_errors(self.h, self._stream())
+        if v < 0:
+            raise capi.LsmError("lsm_action_errors failed")
+        if v:
+            raise ValueError("an action index outside [0, 25) (Discrete(25)) reached the rollout")
 
     def step(self, actions, num_current_episode: Optional[int] = None):
         self.step_async(actions, num_current_episode)

@@ -89,25 +89,29 @@ class Grid:
                 idx_lo[d] = f
                 idx_hi[d] = f + 1
         w_lo = (F32(1.0) - w_hi).astype(F32)
-        strides = self.strides
-        flat = []
-        wts = []
-        for c in range(1 << self.ndim):
-            w = None
-            off = 0
-            for d in range(self.ndim):
-                bit = (c >> (self.ndim - 1 - d)) & 1
-                wd = w_hi[d] if bit else w_lo[d]
-                w = wd if w is None else F32(w * wd)
-                off += (idx_hi[d] if bit else idx_lo[d]) * strides[d]
-            flat.append(off)
-            wts.append(w)
-        return np.asarray(flat, dtype=np.int64), np.asarray(wts, dtype=F32)
+        # corner c takes dim d's upper neighbour iff bit (ndim-1-d) of c is set; its weight is
+        # the sequential float32 product over dims (vectorised over corners, same roundings)
+        bits = self._bits()
+        wsel = np.where(bits, w_hi[None, :], w_lo[None, :]).astype(F32)
+        w = wsel[:, 0].copy()
+        for d in range(1, self.ndim):
+            w = (w * wsel[:, d]).astype(F32)
+        flat = (np.where(bits, idx_hi[None, :], idx_lo[None, :]) * np.asarray(self.strides)[None, :]).sum(axis=1)
+        return flat.astype(np.int64), w
+
+    def _bits(self):
+        b = getattr(self, "_bits_cache", None)
+        if b is None:
+            c = np.arange(1 << self.ndim)[:, None]
+            b = ((c >> (self.ndim - 1 - np.arange(self.ndim))[None, :]) & 1).astype(bool)
+            self._bits_cache = b
+        return b
 
     def interpolate(self, values, state):
         """Interpolate ``values`` (grid.shape [+ trailing dims]) at ``state``.
 
-        Returns float32 scalar / vector, NaN(s) when out of domain.
+        Returns float32 scalar / vector, NaN(s) when out of domain. The weighted corners are
+        summed sequentially in float32 (np.cumsum is a running sum).
         """
         values = np.asarray(values)
         trailing = values.shape[self.ndim:]
@@ -115,12 +119,10 @@ class Grid:
         if cw is None:
             return np.full(trailing, np.nan, dtype=F32) if trailing else F32(np.nan)
         flat, wts = cw
-        vflat = values.reshape((-1,) + trailing)
-        acc = np.zeros(trailing, dtype=F32) if trailing else F32(0.0)
-        for k in range(len(flat)):
-            acc = (acc + (wts[k] * vflat[flat[k]]).astype(F32)).astype(F32) if trailing \
-                else F32(acc + F32(wts[k] * vflat[flat[k]]))
-        return acc
+        vflat = values.reshape((-1,) + trailing)[flat]
+        prod = (wts.reshape((-1,) + (1,) * len(trailing)) * vflat).astype(F32)
+        acc = np.cumsum(prod, axis=0, dtype=F32)[-1]
+        return acc if trailing else F32(acc)
 
     # -- gradients -------------------------------------------------------------
     def grad_values(self, values):

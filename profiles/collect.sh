@@ -31,6 +31,7 @@ run sq2 --pmc SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_AC
 
 cd "$ROOT/layered-safe-marl_amd"
 python -m lsm.pmc stats "$OUT/ktrace" > "$ROOT/profiles/${ROUND}_config${CFG}_kernel_stats.txt"
+python -m lsm.pmc launches "$OUT/ktrace" --kernel "$KERN" > "$ROOT/profiles/${ROUND}_config${CFG}_launches.json"
 cp "$(find "$OUT/ktrace" -name '*kernel_stats.csv' | head -n1)" "$ROOT/profiles/${ROUND}_config${CFG}_kernel_stats.csv"
 python -m lsm.pmc traffic "$OUT/fetch" "$OUT/write" --config "$CFG" --envs "$ENVS" --kernel "$KERN" \
     --out "$ROOT/profiles/pmc_traffic.json" > "$ROOT/profiles/${ROUND}_config${CFG}_traffic.json"

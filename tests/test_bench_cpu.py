@@ -13,10 +13,52 @@ def test_cpu_baseline_leg_small_sample():
 
 
 def test_step_bytes_model():
+    """record (read whole, hot part written) + outputs + HJ gathers (64 B per ordered
+    agent pair + 256 B per ego for the 4-D table)."""
     d = step_bytes(8, 2, "double_integrator", True, "reference")
-    assert d["hbm_bytes"] == 31753 and d["gather_bytes"] == 5632 and not d["block"]
+    assert d["gather_bytes"] == 64 * 8 * 7 + 256 * 8 == 5632 and not d["block"]
+    assert d["hbm_bytes"] == d["state"] + d["outputs"] + d["gather_bytes"] == 37465   # state incl. actions
+    assert step_bytes(8, 2, "double_integrator", False)["gather_bytes"] == 0
     d = step_bytes(64, 2, "double_integrator", True, "compact")
-    assert d["block"] and d["E"] == 192 and d["hbm_bytes"] == 680897
+    assert d["block"] and d["E"] == 192 and d["hbm_bytes"] == 955409
+    d = step_bytes(16, 2, "airtaxi", True, "reference")
+    assert d["gather_bytes"] == 128 * 16 * 15 + 32 * 32 * 16
+
+
+def test_timed_window_straddles_an_episode_boundary():
+    for w, k, epl in ((5, 20, 250), (250, 1000, 250), (0, 1, 350), (3, 7, 10), (100, 2, 250)):
+        pre = bench.timed_window(w, k, epl)
+        assert pre >= w
+        boundaries = [t for t in range(pre, pre + k) if (t + 1) % epl == 0]
+        assert boundaries or k < 2, (w, k, epl, pre)
+
+
+def test_multi_rank_launch_dry_run():
+    """bench.py --gpus 2 starts two rank processes itself (no torchrun): each sees WORLD_SIZE=2, owns
+    the env block [r * n, (r + 1) * n) and joins the episode-summary collective (gloo here)."""
+    import json
+    import subprocess
+    import sys
+    out = subprocess.run([sys.executable, bench.__file__, "--gpus", "2", "--dry-run", "--envs", "8",
+                          "--steps", "20", "--warmup", "5"], capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, out.stderr[-2000:]
+    line = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["world_size"] == 2
+    assert [(r["rank"], r["env_offset"], r["envs"]) for r in line["ranks"]] == [(0, 0, 8), (1, 8, 8)]
+    assert line["max_over_ranks"] == 2.0
+    # mean over both ranks' 16 envs of arange rows
+    assert line["episode_summary"]["travel_time_mean"] == 60.0
+    assert line["untimed_steps"] == 240
+
+
+def test_world_size_must_match_gpus():
+    import os
+    import subprocess
+    import sys
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    out = subprocess.run([sys.executable, bench.__file__, "--gpus", "2", "--dry-run"], capture_output=True,
+                         text=True, timeout=120, env=env)
+    assert out.returncode != 0 and "WORLD_SIZE" in (out.stderr + out.stdout)
 
 
 def test_traffic_lookup_matches_workload():

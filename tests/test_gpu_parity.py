@@ -111,6 +111,12 @@ CASES = [
          num_env_steps=80 * 4, use_safety_filter=True, ep=4),
     dict(dynamics_type="airtaxi", num_agents=4, world_size=6, episode_length=80,
          num_env_steps=80 * 4, use_safety_filter=False, ep=2),
+    # BASELINE config 4's env: 16 airtaxi agents (E = 48), filter on -> rollout_kernel<1, 64, 16>
+    dict(dynamics_type="airtaxi", num_agents=16, world_size=6, episode_length=20,
+         num_env_steps=20 * 4, use_safety_filter=True, ep=4, n_envs=8),
+    # compile-time N = 8 / N = 3 double integrator (rollout_kernel<0, 64, 8> / <0, 64, 3>)
+    dict(dynamics_type="double_integrator", num_agents=3, world_size=4, episode_length=60,
+         num_env_steps=60 * 4, use_safety_filter=True, ep=4),
 ]
 
 
@@ -121,6 +127,8 @@ def test_gpu_matches_oracle_multi_env(case, lpe, monkeypatch):
     actions, across an auto-reset; every kernel variant: 1, 2 or 4 envs/wave, at one env
     per wave both the compile-time-N kernel (N = 3, 8, 16) and the generic one ("64g"), and
     the workgroup-per-env kernel in both adjacency layouts ("block", "blockc")."""
+    if lpe == 16 and CASES[case]["num_agents"] == 16 and CASES[case]["dynamics_type"] == "airtaxi":
+        pytest.skip("4 airtaxi envs of 16 agents per wave need 98 KB of LDS (> 64 KB per workgroup)")
     layout = "reference"
     if lpe in ("block", "blockc"):
         monkeypatch.setenv("LSM_KERNEL", "block")
@@ -132,9 +140,10 @@ def test_gpu_matches_oracle_multi_env(case, lpe, monkeypatch):
     monkeypatch.setenv("LSM_LPE", str(lpe))
     c = dict(CASES[case])
     ep = c.pop("ep")
+    nb = c.pop("n_envs", 16)   # the oracle takes ~36 ms per 16-agent airtaxi env-step
     meta = dict(num_landmarks=2, n_rollout_threads=1, use_masking=True, num_internal_step=1, seed=5,
                 env_seed=5, **c)
-    n_envs, steps = (16 if lpe == 64 else 15), min(c["episode_length"] + 20, 120)
+    n_envs, steps = (nb if lpe == 64 else nb - 1), min(c["episode_length"] + 20, 120)
     env = _gpu_env(meta, n_envs=n_envs, seed=5, adj_layout=layout)
     ora = _oracle_for(meta, 5, n_envs)
     g = env.reset(ep)
@@ -468,4 +477,75 @@ def test_gpu_separation_chain_bound():
         env.reset(12)
     env._upload_value_table()
     env.reset(12)
+    env.close()
+
+
+def test_gpu_config4_full_size_properties_and_sampled_oracle():
+    """BASELINE config 4 (16 airtaxi agents x 8192 envs, HJ filter on, episode_length 350):
+    rollout_kernel<1, 64, 16> over 360 steps spanning the auto-reset at step 350: invariants
+    every 20 steps and around the reset, and sampled envs replayed exactly through the oracle."""
+    import torch
+    meta = dict(dynamics_type="airtaxi", num_agents=16, num_landmarks=2, world_size=6,
+                episode_length=350, num_env_steps=350 * 4, n_rollout_threads=1, use_safety_filter=True,
+                use_masking=True, num_internal_step=1, seed=0, env_seed=0)
+    n_envs, N, E = 8192, 16, 48
+    env = _gpu_env(meta, n_envs=n_envs, seed=0, return_numpy=False)
+    sample = [0, 8191]   # the oracle takes ~36 ms per env-step here
+    oras = [_oracle_for(meta, 0, 1, env_offset=k) for k in sample]
+    obs, aid, node, adj, ep = env.reset(4)
+    assert node.shape == (n_envs, N, E, 11) and adj.shape == (n_envs, N, E, E)
+    for k, o in zip(sample, oras):
+        r = o.reset(4)
+        np.testing.assert_allclose(obs[k].cpu().numpy(), r[0][0], rtol=0, atol=F32_ATOL)
+    gen = torch.Generator(device="cuda:0").manual_seed(4)
+    vmin, vmax = 60 * 0.514444 * 0.001, 175 * 0.514444 * 0.001
+    for t in range(360):
+        a = torch.randint(0, 25, (n_envs, N), device="cuda:0", generator=gen, dtype=torch.int32)
+        obs, aid, node, adj, rew, dones, (info, reset, epinfo) = env.step(a, 4)
+        st = env.state()
+        if t % 20 == 0 or t >= 348:
+            assert torch.isfinite(obs).all() and torch.isfinite(node).all() and torch.isfinite(adj).all()
+            assert (adj >= 0).all() and (adj <= 3 * 1.60934 + 1e-6).all()
+            assert (torch.diagonal(adj, dim1=2, dim2=3) == 0).all()
+            assert torch.equal(adj, adj.transpose(2, 3))
+            live = ~dones
+            spd = st[..., 3]
+            assert ((spd >= vmin - 1e-15) & (spd <= vmax + 1e-15) | ~live).all()
+            assert (rew >= -40).all() and (rew <= 50).all()
+        if t == 349:
+            assert bool(reset.all())
+        a_h = a.cpu().numpy()
+        for k, o in zip(sample, oras):
+            r = o.step(a_h[k:k + 1], 4)
+            ctx = "env %d step %d" % (k, t)
+            np.testing.assert_array_equal(dones[k].cpu().numpy(), r[5][0], err_msg=ctx)
+            np.testing.assert_array_equal((adj[k] != 0).cpu().numpy(), r[3][0] != 0, err_msg=ctx)
+            np.testing.assert_allclose(obs[k].cpu().numpy(), r[0][0], rtol=0, atol=F32_ATOL, err_msg=ctx)
+            np.testing.assert_allclose(rew[k].cpu().numpy(), r[4][0], rtol=1e-6, atol=1e-5, err_msg=ctx)
+            np.testing.assert_allclose(st[k].cpu().numpy(), o.envs[0].s, rtol=0, atol=STATE_ATOL, err_msg=ctx)
+            if t % 50 == 0:
+                np.testing.assert_allclose(node[k].cpu().numpy(), r[2][0], rtol=0, atol=F32_ATOL, err_msg=ctx)
+                np.testing.assert_allclose(adj[k].cpu().numpy(), r[3][0], rtol=0, atol=F32_ATOL, err_msg=ctx)
+    env.close()
+
+
+def test_gpu_action_index_out_of_range_is_reported():
+    """Index actions outside Discrete(25): host arrays are refused before launch; a device tensor
+    is clamped in the kernel (the launch stays in bounds) and reported by check_actions()."""
+    import torch
+    meta = dict(dynamics_type="double_integrator", num_agents=3, num_landmarks=2, world_size=4,
+                episode_length=20, num_env_steps=20 * 4, n_rollout_threads=1, use_safety_filter=False,
+                use_masking=True, num_internal_step=1, seed=1, env_seed=1)
+    env = _gpu_env(meta, n_envs=4, seed=1, return_numpy=False)
+    env.reset(2)
+    with pytest.raises(ValueError):
+        env.step(np.full((4, 3), 25), 2)
+    env.step(torch.zeros((4, 3), dtype=torch.int32, device="cuda:0"), 2)
+    env.check_actions()                                   # nothing flagged
+    bad = torch.zeros((4, 3), dtype=torch.int32, device="cuda:0")
+    bad[2, 1] = -3
+    env.step(bad, 2)
+    with pytest.raises(ValueError, match="outside"):
+        env.check_actions()
+    env.check_actions()                                   # the flag was cleared
     env.close()
