@@ -68,7 +68,9 @@ enum {
   LSM_OUT_SHARE_OBS = 12, /* float32 [n][N][N*OBS] centralized share_obs (obs row per agent) */
   LSM_OUT_MASKS = 13,     /* float32 [n][N]   1 - done                                   */
   LSM_OUT_ACTIVE_MASKS = 14, /* float32 [n][N] done ? all(env dones) : 1                 */
-  LSM_NUM_OUT = 15
+  LSM_OUT_COLLISION_FORCE = 15, /* float64 [n][N][2] contact force per agent, written only with
+                                   lsm_config.collision_forces (core.py:741-774; never applied) */
+  LSM_NUM_OUT = 16
 };
 
 /* Adjacency output layouts (lsm_config.adj_layout).
@@ -104,6 +106,10 @@ typedef struct lsm_config {
   double world_size;         /* args.world_size                                        */
   int64_t seed;              /* env k (global index env_offset + k) seeded seed+1000*k */
   int64_t env_offset;
+  int32_t collision_forces;  /* 1: report World.get_entity_collision_force per agent each step
+                                (LSM_OUT_COLLISION_FORCE). The reference has no caller for it
+                                (core.py:741-836), so it never changes the dynamics. Default 0. */
+  int32_t reserved0;
 } lsm_config;
 
 /* Curriculum block for one reset call (navigation_graph_safe.py:324-366), computed by the

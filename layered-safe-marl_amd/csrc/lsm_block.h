@@ -403,6 +403,13 @@ __global__ __launch_bounds__(BT) void rollout_block_kernel(const KParams* __rest
   if (tid < N && !S.dpre[tid]) integrate_agent<DYN>(P, S, N, tid);
   __syncthreads();
   STAMP(5);
+  if (P.o.cforce && tid < N) {   // optional contact forces (collision_force_agent)
+    double fx, fy;
+    collision_force_agent(S, N, tid, fx, fy);
+    GAS double* cf = gptr(P.o.cforce) + ((size_t)env * N + tid) * 2;
+    cf[0] = fx;
+    cf[1] = fy;
+  }
   entity_table<NT>(P, S);
 
   // ---- 5. min relative distance (active agents) and is_collision counts (all agents) ------

@@ -97,26 +97,6 @@ LSM_RK_HD double glibc_pow(double x, double y) {
   return glibc_exp_inline(ehi, elo);
 }
 
-// np.dot(K[:s].T, w) for K rows of 4 (OpenBLAS dgemv_n column groups, see above)
-LSM_RK_HD void rk_gemv(const double (*K)[4], const double* w, int s, double* out) {
-  for (int r = 0; r < 4; ++r) {
-    double y = 0.0;
-    int j = 0;
-    for (; j + 4 <= s; j += 4) {
-      double t = fma(K[j][r], w[j], K[j + 1][r] * w[j + 1]);
-      t = fma(K[j + 2][r], w[j + 2], t);
-      t = fma(K[j + 3][r], w[j + 3], t);
-      y = y + t;
-    }
-    if ((s - j) & 2) {
-      y = y + fma(K[j][r], w[j], K[j + 1][r] * w[j + 1]);
-      j += 2;
-    }
-    if ((s - j) & 1) y = y + K[j][r] * w[j];
-    out[r] = y;
-  }
-}
-
 // scipy common.norm: np.linalg.norm(x) / sqrt(x.size) for a 4-vector (ddot fma chain)
 LSM_RK_HD double rk_norm4(const double* x) {
   double s = x[0] * x[0];
@@ -143,25 +123,80 @@ LSM_RK_HD const Rk45Tab& rk45_tab() {
   return T;
 }
 
+// One velocity component's np.dot(K[:s].T, w) when every stage row holds the same value a
+// (the accelerations: K[j][2] = a0, K[j][3] = a1 for all j): OpenBLAS dgemv_n column groups.
+LSM_RK_HD double rk_gemv_const(double a, const double* w, int s) {
+  double y = 0.0;
+  int j = 0;
+  for (; j + 4 <= s; j += 4) {
+    double t = fma(a, w[j], a * w[j + 1]);
+    t = fma(a, w[j + 2], t);
+    t = fma(a, w[j + 3], t);
+    y = y + t;
+  }
+  if ((s - j) & 2) {
+    y = y + fma(a, w[j], a * w[j + 1]);
+    j += 2;
+  }
+  if ((s - j) & 1) y = y + a * w[j];
+  return y;
+}
+
+// One position component's np.dot(K[:s].T, w): K[j] = the stage velocities k[j].
+LSM_RK_HD double rk_gemv_col(const double* k, const double* w, int s) {
+  double y = 0.0;
+  int j = 0;
+  for (; j + 4 <= s; j += 4) {
+    double t = fma(k[j], w[j], k[j + 1] * w[j + 1]);
+    t = fma(k[j + 2], w[j + 2], t);
+    t = fma(k[j + 3], w[j + 3], t);
+    y = y + t;
+  }
+  if ((s - j) & 2) {
+    y = y + fma(k[j], w[j], k[j + 1] * w[j + 1]);
+    j += 2;
+  }
+  if ((s - j) & 1) y = y + k[j] * w[j];
+  return y;
+}
+
 // solve_ivp(x' = v, v' = a, [0, tb], y, method='RK45').y[:, -1] (rtol 1e-3, atol 1e-6, no
-// max_step). Returns the number of steps; y is updated in place. A rejected step (error norm
-// >= 1, which this polynomial ODE does not produce) returns -1 with y unchanged.
+// max_step), y updated in place, returns the number of steps. Same operations and roundings as
+// scipy's generic code (dgemv over the K rows), specialised to this ODE:
+//   * the right-hand side ignores positions, so the stage positions y + dy (dy[0], dy[1]) feed
+//     nothing and are not formed;
+//   * K[j][2..3] = a for every stage, so the velocity-component dot products depend on a only and
+//     are computed once per call instead of once per step;
+//   * the error factor min(10, 0.9 err^-1/5) is 10 without evaluating pow when err <= 1e-6
+//     (0.9 * (1e-6)^-0.2 = 14.2 > 10); err == 0 gives 10 as in scipy.
+// A rejected step (err >= 1) follows _step_impl: h *= max(0.2, 0.9 err^-1/5), factor <= 1 after.
 LSM_RK_HD int rk45_di(double* y, double a0, double a1, double tb) {
   const double rtol = 1e-3, atol = 1e-6;
   const Rk45Tab& T = rk45_tab();
-  double f[4] = {y[2], y[3], a0, a1};
-  double sc[4], tmp[4];
+  // velocity-component stage increments, final combination and error dot products
+  double dv0[6], dv1[6];
+#pragma unroll
+  for (int s = 1; s < 6; ++s) {
+    dv0[s] = rk_gemv_const(a0, T.A[s], s);
+    dv1[s] = rk_gemv_const(a1, T.A[s], s);
+  }
+  const double gb0 = rk_gemv_const(a0, T.B, 6), gb1 = rk_gemv_const(a1, T.B, 6);
+  const double ge0 = rk_gemv_const(a0, T.E, 7), ge1 = rk_gemv_const(a1, T.E, 7);
   // select_initial_step
-  for (int i = 0; i < 4; ++i) sc[i] = atol + fabs(y[i]) * rtol;
-  for (int i = 0; i < 4; ++i) tmp[i] = y[i] / sc[i];
-  const double d0 = rk_norm4(tmp);
-  for (int i = 0; i < 4; ++i) tmp[i] = f[i] / sc[i];
-  const double d1 = rk_norm4(tmp);
+  const double sc0 = atol + fabs(y[0]) * rtol, sc1 = atol + fabs(y[1]) * rtol;
+  const double sc2 = atol + fabs(y[2]) * rtol, sc3 = atol + fabs(y[3]) * rtol;
+  double t4[4] = {y[0] / sc0, y[1] / sc1, y[2] / sc2, y[3] / sc3};
+  const double d0 = rk_norm4(t4);
+  t4[0] = y[2] / sc0; t4[1] = y[3] / sc1; t4[2] = a0 / sc2; t4[3] = a1 / sc3;
+  const double d1 = rk_norm4(t4);
   double h0 = (d0 < 1e-5 || d1 < 1e-5) ? 1e-6 : 0.01 * d0 / d1;
   h0 = (tb < h0) ? tb : h0;
-  const double f1[4] = {y[2] + h0 * f[2], y[3] + h0 * f[3], a0, a1};
-  for (int i = 0; i < 4; ++i) tmp[i] = (f1[i] - f[i]) / sc[i];
-  const double d2 = rk_norm4(tmp) / h0;
+  // f1 - f0 = [(v + h0 a) - v, 0, 0] per axis (f1 of y0 + h0 f0)
+  t4[0] = ((y[2] + h0 * a0) - y[2]) / sc0;
+  t4[1] = ((y[3] + h0 * a1) - y[3]) / sc1;
+  t4[2] = (a0 - a0) / sc2;
+  t4[3] = (a1 - a1) / sc3;
+  const double d2 = rk_norm4(t4) / h0;
   double h1;
   if (d1 <= 1e-15 && d2 <= 1e-15) {
     h1 = (h0 * 1e-3 > 1e-6) ? h0 * 1e-3 : 1e-6;
@@ -172,43 +207,54 @@ LSM_RK_HD int rk45_di(double* y, double a0, double a1, double tb) {
   if (h1 < h_abs) h_abs = h1;
   if (tb < h_abs) h_abs = tb;
   double t = 0.0;
-  double K[7][4];
   int n = 0;
+  double v0 = y[2], v1 = y[3];       // K[0][0..1] = f[0..1] = the step's starting velocity
   while (t < tb) {
-    double t_new = t + h_abs;
-    if (t_new - tb > 0) t_new = tb;
-    const double h = t_new - t;
-    h_abs = fabs(h);
-    for (int i = 0; i < 4; ++i) K[0][i] = f[i];
-    for (int s = 1; s < 6; ++s) {
-      double dy[4];
-      rk_gemv(K, T.A[s], s, dy);
-      K[s][0] = y[2] + dy[2] * h;   // fun(t + c h, y + dy * h) = [vx, vy, a0, a1]
-      K[s][1] = y[3] + dy[3] * h;
-      K[s][2] = a0;
-      K[s][3] = a1;
+    bool rejected = false;
+    for (;;) {
+      double t_new = t + h_abs;
+      if (t_new - tb > 0) t_new = tb;
+      const double h = t_new - t;
+      h_abs = fabs(h);
+      double k0[7], k1[7];           // stage velocities (the position components of K)
+      k0[0] = v0; k1[0] = v1;
+#pragma unroll
+      for (int s = 1; s < 6; ++s) {
+        k0[s] = y[2] + dv0[s] * h;
+        k1[s] = y[3] + dv1[s] * h;
+      }
+      const double yn0 = y[0] + h * rk_gemv_col(k0, T.B, 6);
+      const double yn1 = y[1] + h * rk_gemv_col(k1, T.B, 6);
+      const double yn2 = y[2] + h * gb0;
+      const double yn3 = y[3] + h * gb1;
+      k0[6] = yn2; k1[6] = yn3;
+      const double e0 = rk_gemv_col(k0, T.E, 7), e1 = rk_gemv_col(k1, T.E, 7);
+      double r4[4];
+      const double yy[4] = {y[0], y[1], y[2], y[3]}, yn[4] = {yn0, yn1, yn2, yn3}, ee[4] = {e0, e1, ge0, ge1};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const double ay = fabs(yy[i]), ayn = fabs(yn[i]);
+        r4[i] = (ee[i] * h) / (atol + ((ay >= ayn) ? ay : ayn) * rtol);
+      }
+      const double en = rk_norm4(r4);
+      if (en < 1) {
+        double fac = 10.0;           // MAX_FACTOR
+        if (en > 1e-6) {
+          const double q = 0.9 * glibc_pow(en, -1.0 / 5.0);
+          if (q < fac) fac = q;
+        }
+        if (rejected && fac > 1) fac = 1;
+        h_abs *= fac;
+        t = t_new;
+        y[0] = yn0; y[1] = yn1; y[2] = yn2; y[3] = yn3;
+        v0 = yn2; v1 = yn3;
+        ++n;
+        break;
+      }
+      const double q = 0.9 * glibc_pow(en, -1.0 / 5.0);
+      h_abs *= (q > 0.2) ? q : 0.2;
+      rejected = true;
     }
-    double g[4], yn[4];
-    rk_gemv(K, T.B, 6, g);
-    for (int i = 0; i < 4; ++i) yn[i] = y[i] + h * g[i];
-    K[6][0] = yn[2]; K[6][1] = yn[3]; K[6][2] = a0; K[6][3] = a1;
-    double e[4];
-    rk_gemv(K, T.E, 7, e);
-    for (int i = 0; i < 4; ++i) {
-      const double ay = fabs(y[i]), ayn = fabs(yn[i]);
-      tmp[i] = (e[i] * h) / (atol + ((ay >= ayn) ? ay : ayn) * rtol);
-    }
-    const double en = rk_norm4(tmp);
-    if (!(en < 1)) return -1;
-    double fac = 10.0;   // MAX_FACTOR
-    if (en != 0) {
-      const double q = 0.9 * glibc_pow(en, -1.0 / 5.0);   // SAFETY * error_norm ** error_exponent
-      if (q < fac) fac = q;
-    }
-    h_abs *= fac;
-    t = t_new;
-    for (int i = 0; i < 4; ++i) { y[i] = yn[i]; f[i] = K[6][i]; }
-    ++n;
   }
   return n;
 }

@@ -132,6 +132,7 @@ struct OutDev {
   float* share_obs;    // LSM_OUT_SHARE_OBS (optional)
   float* masks;        // LSM_OUT_MASKS (optional)
   float* active_masks; // LSM_OUT_ACTIVE_MASKS (optional)
+  double* cforce;      // LSM_OUT_COLLISION_FORCE (lsm_config.collision_forces only)
 };
 
 struct KParams {
@@ -1757,6 +1758,39 @@ __device__ __forceinline__ void integrate_agent(const KParams& P, Lds& S, int N,
   S.pdist[i] += spd * dt;
 }
 
+// numpy's logaddexp(0, z) (npy_logaddexp: x + log1p(exp(y - x)) around the larger argument)
+__device__ __forceinline__ double np_logaddexp0(double z) {
+  if (z == 0.0) return 0.693147180559945309417232121458176568;   // NPY_LOGE2
+  const double tmp = 0.0 - z;
+  if (tmp > 0) return 0.0 + log1p(exp(-tmp));
+  return z + log1p(exp(tmp));
+}
+
+// Optional (lsm_config.collision_forces, off by default): the contact force on agent i that the
+// reference's World.get_entity_collision_force (core.py:741-774) returns for each agent pair,
+// summed over the pairs in order as MPE's apply_environment_force accumulates it (p_force[a] =
+// f_a + p_force[a]). The reference never calls it (no caller, SURVEY finding 1), so the rollout
+// does not apply it; this reports it. Fresh post-integration distances (World.step's
+// calculate_distances, core.py:626), done flags as World.step sees them (force_a is None for a
+// done agent -> 0); landmarks do not collide (navigation_graph_safe.py:52). Masses are 1, so
+// both members of a pair get +-130 (p_a - p_b) / d * penetration and every agent's terms are
+// +130 (p_i - p_j) / d * penetration, j in increasing order. Transcendentals are the device's
+// (ulp-level vs glibc exp / log1p); nothing downstream reads the result.
+__device__ __forceinline__ void collision_force_agent(const Lds& S, int N, int i, double& fx, double& fy) {
+  fx = 0.0;
+  fy = 0.0;
+  if (S.dpre[i]) return;
+  const double k = 1.9e-3, dmin = 0.050 + 0.050;   // contact_margin, min_dists (core.py:400, 524-530)
+  for (int j = 0; j < N; ++j) {
+    if (j == i) continue;
+    const double dx = S.ps[i] - S.ps[j], dy = S.ps[N + i] - S.ps[N + j];
+    const double dist = sqrt(dx * dx + dy * dy);
+    const double pen = np_logaddexp0(-(dist - dmin) / k) * k;
+    fx = 1.3e+2 * dx / dist * pen + fx;
+    fy = 1.3e+2 * dy / dist * pen + fy;
+  }
+}
+
 // Per-agent values of the reward phase that the info phase reuses.
 struct AgentTmp {
   double rew = 0.0, th_pre = 0.0, spd_pre = 0.0, ct_pre = 1.0, st_pre = 0.0;
@@ -1932,8 +1966,14 @@ __device__ __forceinline__ void stats_agent(const KParams& P, Lds& S, int N, int
   }
 }
 
+// Double integrator: 4 waves per SIMD (<= 128 VGPRs): config 3 is exactly 4096 one-wave envs =
+// 4 per SIMD, and at 134 VGPRs the 4th wave of every SIMD ran after the others (53 vs 41 us per
+// step, measured). Airtaxi keeps 2 (~176 VGPRs; a 128 cap spills 200-350 B per lane).
+#ifndef LSM_WAVES_PER_EU_AT
+#define LSM_WAVES_PER_EU_AT 2
+#endif
 template <int DYN, int LPE, int NT>
-__global__ __launch_bounds__(64) void rollout_kernel(const KParams* __restrict__ Pp, const KStep K) {
+__global__ __launch_bounds__(64, DYN == 0 ? (LPE == 64 ? 4 : 2) : LSM_WAVES_PER_EU_AT) void rollout_kernel(const KParams* __restrict__ Pp, const KStep K) {
   const KParams& P = *Pp;   // per-handle constants in device memory; per-launch fields in L
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int G = WAVE / LPE;   // envs per wave, one per LPE-lane group
@@ -2085,6 +2125,13 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KParams* __restrict__
 
   // ---- 5. distances, min relative distance ---------------------------------------------
   compute_dist<LPE, NT>(P, S, PRE ? prw : nullptr);
+  if (P.o.cforce && lane < N) {
+    double fx, fy;
+    collision_force_agent(S, N, lane, fx, fy);
+    GAS double* cf = gptr(P.o.cforce) + ((size_t)env * N + lane) * 2;
+    cf[0] = fx;
+    cf[1] = fy;
+  }
   if (lane < N) {
     const int i = lane;
     double m = INFINITY;
@@ -2336,6 +2383,7 @@ static void fill_params(const lsm_env* e, KParams& P) {
   P.o.share_obs = (float*)e->out_ptr[LSM_OUT_SHARE_OBS];
   P.o.masks = (float*)e->out_ptr[LSM_OUT_MASKS];
   P.o.active_masks = (float*)e->out_ptr[LSM_OUT_ACTIVE_MASKS];
+  P.o.cforce = e->cfg.collision_forces ? (double*)e->out_ptr[LSM_OUT_COLLISION_FORCE] : nullptr;
   P.stamps = (unsigned long long*)e->out_ptr[LSM_OUT_DEBUG_STAMPS];
   P.diag = 0;
 #ifdef LSM_STAMPS
@@ -2365,6 +2413,7 @@ size_t lsm_output_bytes(const lsm_env* e, int32_t slot) {
     case LSM_OUT_SHARE_OBS: return n * N * N * e->OBS * 4;
     case LSM_OUT_MASKS: return n * N * 4;
     case LSM_OUT_ACTIVE_MASKS: return n * N * 4;
+    case LSM_OUT_COLLISION_FORCE: return n * N * 2 * 8;
     default: return 0;
   }
 }
@@ -2662,6 +2711,8 @@ static int check_ready(lsm_env* e, bool stepping) {
     if (!e->out_ptr[s]) return fail(e, "output slot " + std::to_string(s) + " not bound");
   if (e->cfg.adj_layout == LSM_ADJ_COMPACT && !e->out_ptr[LSM_OUT_ADJ_MASK])
     return fail(e, "compact adjacency layout needs LSM_OUT_ADJ_MASK bound");
+  if (e->cfg.collision_forces && !e->out_ptr[LSM_OUT_COLLISION_FORCE])
+    return fail(e, "collision_forces needs LSM_OUT_COLLISION_FORCE bound");
   (void)stepping;
   return 0;
 }
@@ -2704,6 +2755,7 @@ static void apply_ring(const lsm_env* e, int i, KParams& P) {
   P.o.share_obs = (float*)at(LSM_OUT_SHARE_OBS, P.o.share_obs);
   P.o.masks = (float*)at(LSM_OUT_MASKS, P.o.masks);
   P.o.active_masks = (float*)at(LSM_OUT_ACTIVE_MASKS, P.o.active_masks);
+  P.o.cforce = (double*)at(LSM_OUT_COLLISION_FORCE, P.o.cforce);
 }
 
 extern "C++" template <int DYN, int LPE, int NT>
@@ -2769,7 +2821,10 @@ static int launch(lsm_env* e, KStep& L, hipStream_t st) {
   // specialised kernels (compile-time N, L = 2, one env per wave) for the BASELINE agent
   // counts; everything else runs the generic kernel (runtime dims, LPE 64/32/16)
   const bool spec = e->lpe == 64 && e->L == 2 && !e->generic_only;
-  if (spec && di && e->N == 3) launch_t<0, 64, 3>(e, L, env_lds, st);
+  const bool spec32 = e->lpe == 32 && e->L == 2 && !e->generic_only;
+  if (spec32 && di && e->N == 8) launch_t<0, 32, 8>(e, L, env_lds, st);
+  else if (spec32 && !di && e->N == 16) launch_t<1, 32, 16>(e, L, env_lds, st);
+  else if (spec && di && e->N == 3) launch_t<0, 64, 3>(e, L, env_lds, st);
   else if (spec && di && e->N == 8) launch_t<0, 64, 8>(e, L, env_lds, st);
   else if (spec && !di && e->N == 3) launch_t<1, 64, 3>(e, L, env_lds, st);
   else if (spec && !di && e->N == 16) launch_t<1, 64, 16>(e, L, env_lds, st);

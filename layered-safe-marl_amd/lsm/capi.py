@@ -16,8 +16,9 @@ LIB_PATH = os.environ.get("LSM_LIB") or os.path.join(os.path.dirname(_HERE), "cs
 LSM_DOUBLE_INTEGRATOR, LSM_AIRTAXI = 0, 1
 LSM_ACTIONS_INDEX_I32, LSM_ACTIONS_ONEHOT_F32, LSM_ACTIONS_ONEHOT_F64 = 0, 1, 2
 (OUT_OBS, OUT_NODE_OBS, OUT_ADJ, OUT_REWARD, OUT_DONE, OUT_RESET_FLAG, OUT_EP_INFO, OUT_INFO,
- OUT_EDGES, OUT_STATE, OUT_DEBUG_STAMPS, OUT_ADJ_MASK, OUT_SHARE_OBS, OUT_MASKS, OUT_ACTIVE_MASKS) = range(15)
-NUM_OUT = 15
+ OUT_EDGES, OUT_STATE, OUT_DEBUG_STAMPS, OUT_ADJ_MASK, OUT_SHARE_OBS, OUT_MASKS, OUT_ACTIVE_MASKS,
+ OUT_COLLISION_FORCE) = range(16)
+NUM_OUT = 16
 ADJ_REFERENCE, ADJ_COMPACT = 0, 1
 INFO_FIELDS = ("individual_reward", "min_relative_distance", "Dist_to_goal", "Time_req_to_goal",
                "Num_agent_collisions", "Distance_mean", "Distance_variance", "Dists_traveled",
@@ -38,7 +39,8 @@ class LsmConfig(C.Structure):
                 ("num_landmarks", C.c_int32), ("episode_length", C.c_int32),
                 ("use_safety_filter", C.c_int32), ("use_masking", C.c_int32),
                 ("auto_reset", C.c_int32), ("emit_edges", C.c_int32), ("adj_layout", C.c_int32),
-                ("world_size", C.c_double), ("seed", C.c_int64), ("env_offset", C.c_int64)]
+                ("world_size", C.c_double), ("seed", C.c_int64), ("env_offset", C.c_int64),
+                ("collision_forces", C.c_int32), ("reserved0", C.c_int32)]
 
 
 class LsmCurriculum(C.Structure):

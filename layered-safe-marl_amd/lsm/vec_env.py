@@ -94,7 +94,7 @@ class GpuGraphVecEnv:
                  value_table: Optional[HjTable] = None, ttr_table: Optional[HjTable] = None,
                  auto_reset: bool = True, env_offset: int = 0, emit_edges: bool = False,
                  return_numpy: bool = True, build_infos: bool = True, small_tables: bool = False,
-                 adj_layout: str = "reference"):
+                 adj_layout: str = "reference", collision_forces: bool = False):
         torch = _torch()
         self.args = EnvArgs.from_namespace(all_args) if not isinstance(all_args, EnvArgs) else all_args
         self.args.validate()
@@ -122,7 +122,8 @@ class GpuGraphVecEnv:
                              emit_edges=int(bool(emit_edges)),
                              adj_layout=capi.ADJ_COMPACT if adj_layout == "compact" else capi.ADJ_REFERENCE,
                              world_size=float(a.world_size),
-                             seed=int(a.seed), env_offset=int(env_offset))
+                             seed=int(a.seed), env_offset=int(env_offset),
+                             collision_forces=int(bool(collision_forces)))
         if int(a.seed) + 1000 * (int(env_offset) + self.num_envs - 1) >= 2 ** 32:
             raise ValueError("numpy seeds must be < 2**32 (seed + 1000 * env index)")
         h = C.c_void_p()
@@ -163,12 +164,14 @@ class GpuGraphVecEnv:
         self.t_info = torch.zeros((n, N, len(capi.INFO_FIELDS)), dtype=torch.float64, device=dev)
         self.t_state = torch.zeros((n, N, 4), dtype=torch.float64, device=dev)
         self.t_edges = torch.zeros((n, E, E), dtype=torch.uint8, device=dev) if emit_edges else None
+        # World.get_entity_collision_force per agent (optional report; never applied, like the reference)
+        self.t_cforce = torch.zeros((n, N, 2), dtype=torch.float64, device=dev) if collision_forces else None
         for slot, t in ((capi.OUT_OBS, self.t_obs), (capi.OUT_NODE_OBS, self.t_node),
                         (capi.OUT_ADJ, self.t_adj), (capi.OUT_REWARD, self.t_rew),
                         (capi.OUT_DONE, self.t_done), (capi.OUT_RESET_FLAG, self.t_reset),
                         (capi.OUT_EP_INFO, self.t_epinfo), (capi.OUT_INFO, self.t_info),
                         (capi.OUT_STATE, self.t_state), (capi.OUT_EDGES, self.t_edges),
-                        (capi.OUT_ADJ_MASK, self.t_adj_mask)):
+                        (capi.OUT_ADJ_MASK, self.t_adj_mask), (capi.OUT_COLLISION_FORCE, self.t_cforce)):
             if t is None:
                 continue
             capi.check(self.lib.lsm_bind_output(h, slot, C.c_void_p(t.data_ptr()),

@@ -180,6 +180,8 @@ class OracleEnv:
         self.di = g("dynamics_type") == "double_integrator"
         self.C = _DI if self.di else _AT
         self.integrator = integrator
+        self.report_collision_forces = bool(g("collision_forces", False))
+        self.cforce = np.zeros((self.N, 2))
         C = self.C
         self.dt = C.DT
         self.F = 10 if self.di else 11
@@ -436,6 +438,27 @@ class OracleEnv:
                 dv[a, b, :] = d
                 dv[b, a, :] = -d
         self.cached_dist_mag = np.linalg.norm(dv, axis=2)
+        self.cached_dist_vect = dv
+
+    # ---- contact forces (core.py:397-400, 741-836; no caller in the reference) -------------
+    def collision_forces(self):
+        """Per-agent contact force from World.get_entity_collision_force over every entity pair
+        (ia < ib, core.py:741-774), summed the way MPE's apply_environment_force accumulates them
+        (p_force[a] = f_a + p_force[a], pairs in order), on the distances of the calculate_distances
+        call inside World.step (core.py:626) and the done flags World.step sees. Landmarks do not
+        collide (navigation_graph_safe.py:52), so only agent pairs contribute. Agents with no
+        contribution (done) get 0."""
+        N = self.N
+        tot = [None] * N
+        for a in range(N):
+            for b in range(a + 1, N):
+                fa, fb = entity_collision_force(self.cached_dist_vect[a, b], self.cached_dist_mag[a, b],
+                                                2 * ENTITY_SIZE, bool(self.done[a]), bool(self.done[b]))
+                if fa is not None:
+                    tot[a] = fa + (0.0 if tot[a] is None else tot[a])
+                if fb is not None:
+                    tot[b] = fb + (0.0 if tot[b] is None else tot[b])
+        return np.array([np.zeros(2) if t is None else t for t in tot])
 
     def update_graph(self):
         """navigation_graph_safe.py:996-1015 (row-major COO of the thresholded dists)."""
@@ -799,6 +822,8 @@ class OracleEnv:
                 continue
             self._integrate(i, safe[i])
         self.calculate_distances()
+        if self.report_collision_forces:
+            self.cforce = self.collision_forces()
         M = np.inf * np.ones((self.N, self.N))
         for i in range(self.N):
             if self.done[i] or not self.departed[i]:
@@ -931,6 +956,77 @@ def _rk45_ref():
         lib.rk45_di_ref.restype = ctypes.c_int
         _RK45 = lib
     return _RK45
+
+
+# World contact-response constants (core.py:397-400) and Entity defaults (core.py:261-283)
+CONTACT_FORCE = 1.3e+2
+WALL_CONTACT_FORCE = 2.2e+2
+CONTACT_MARGIN = 1.9e-3
+WALL_CONTACT_MARGIN = 2.4e-2
+ENTITY_SIZE = 0.050
+ENTITY_MASS = 1.0
+
+
+def entity_collision_force(delta_pos, dist, dist_min, a_done, b_done, a_collide=True, b_collide=True,
+                           a_movable=True, b_movable=True, same=False, mass_a=ENTITY_MASS, mass_b=ENTITY_MASS):
+    """World.get_entity_collision_force (core.py:741-774) on the cached distances
+    (cache_dists = True, core.py:414): delta_pos = p_a - p_b, dist = |delta_pos|,
+    dist_min = size_a + size_b (World.min_dists, core.py:524-530). Returns [force_a, force_b],
+    None where the reference returns None."""
+    if (not a_collide) or (not b_collide):
+        return [None, None]
+    if (not a_movable) and (not b_movable):
+        return [None, None]
+    if same:
+        return [None, None]
+    k = CONTACT_MARGIN
+    penetration = np.logaddexp(0, -(dist - dist_min) / k) * k
+    force = CONTACT_FORCE * np.asarray(delta_pos) / dist * penetration
+    if a_movable and b_movable:
+        force_ratio = mass_b / mass_a
+        force_a = force_ratio * force if a_done != True else None   # noqa: E712 (reference test)
+        force_b = -(1 / force_ratio) * force if b_done != True else None   # noqa: E712
+    else:
+        force_a = +force if a_movable else None
+        force_b = -force if b_movable else None
+    return [force_a, force_b]
+
+
+def wall_collision_force(ent_pos, ent_size, wall, ghost=False):
+    """World.get_wall_collision_force (core.py:777-816). wall = (orient 'H'/'V', axis_pos,
+    (endpoint0, endpoint1), width, hard). The training scenario has no walls (num_walls = 0 is
+    required by the graph mask); restated for completeness, pinned by tests/golden/
+    collision_forces.npz."""
+    orient, axis_pos, endpoints, width, hard = wall
+    if ghost and not hard:
+        return None
+    if orient == 'H':
+        prll_dim, perp_dim = 0, 1
+    else:
+        prll_dim, perp_dim = 1, 0
+    ent_pos = np.asarray(ent_pos)
+    if (ent_pos[prll_dim] < endpoints[0] - ent_size or ent_pos[prll_dim] > endpoints[1] + ent_size):
+        return None
+    elif (ent_pos[prll_dim] < endpoints[0] or ent_pos[prll_dim] > endpoints[1]):
+        if ent_pos[prll_dim] < endpoints[0]:
+            dist_past_end = ent_pos[prll_dim] - endpoints[0]
+        else:
+            dist_past_end = ent_pos[prll_dim] - endpoints[1]
+        theta = np.arcsin(dist_past_end / ent_size)
+        dist_min = np.cos(theta) * ent_size + 0.5 * width
+    else:
+        theta = 0
+        dist_past_end = 0
+        dist_min = ent_size + 0.5 * width
+    delta_pos = ent_pos[perp_dim] - axis_pos
+    dist = np.abs(delta_pos)
+    k = WALL_CONTACT_MARGIN
+    penetration = np.logaddexp(0, -(dist - dist_min) / k) * k
+    force_mag = WALL_CONTACT_FORCE * delta_pos / dist * penetration
+    force = np.zeros(2)
+    force[perp_dim] = np.cos(theta) * force_mag
+    force[prll_dim] = np.sin(theta) * np.abs(force_mag)
+    return force
 
 
 class OracleVecEnv:

@@ -187,6 +187,70 @@ def inject_goal_arrival(world, scen):
     world.calculate_distances()
 
 
+def record_collision_forces():
+    """The reference's (dead) contact-force functions, called directly (TEST FIXTURE):
+    World.get_entity_collision_force for every entity pair of a DI world whose agents were placed
+    overlapping / touching / apart (core.py:741-774; one agent done), and
+    World.get_wall_collision_force for an agent at positions around H and V walls (core.py:777-816).
+    None results are stored as NaN."""
+    work = tempfile.mkdtemp(prefix="lsm_ref_")
+    A = ref_harness.default_args
+    env = ref_harness.make_reference_env(A(num_agents=5, num_env_steps=250 * 4), work, 31)
+    ref_harness.run_in(work, env.reset, 2)
+    world = env.world
+    pos = np.array([[0.0, 0.0], [0.08, 0.0], [0.08, 0.12], [0.0, -0.1], [1.5, -2.0]])
+    pos += np.array([0.013, -0.021])   # off the lattice
+    for ag, p in zip(world.agents, pos):
+        ag.state.p_pos = p.copy()
+    world.agents[2].done = True
+    world.calculate_distances()
+    ents = world.entities
+    E = len(ents)
+    forces = np.full((E, E, 2, 2), np.nan)
+    for ia in range(E):
+        for ib in range(ia + 1, E):
+            fa, fb = world.get_entity_collision_force(ia, ib)
+            if fa is not None:
+                forces[ia, ib, 0] = fa
+            if fb is not None:
+                forces[ia, ib, 1] = fb
+    from multiagent.core import Wall
+    walls = [Wall("H", 0.3, (-1.0, 1.0), 0.1, True), Wall("V", -0.4, (-0.5, 0.7), 0.2, True)]
+    wpos = []
+    rng = np.random.default_rng(5)
+    for w in walls:
+        lo, hi = w.endpoints
+        for par in (lo - 0.06, lo - 0.03, lo + 0.2, hi - 0.01, hi + 0.02, hi + 0.049):
+            for off in (-0.2, -0.08, -0.03, 0.0011, 0.04, 0.09, 0.3):
+                p = np.zeros(2)
+                if w.orient == "H":
+                    p[:] = (par, w.axis_pos + off)
+                else:
+                    p[:] = (w.axis_pos + off, par)
+                wpos.append(p + rng.uniform(-1e-3, 1e-3, 2))
+    wpos = np.array(wpos)
+    wforce = np.full((len(walls), len(wpos), 2), np.nan)
+    ag = world.agents[0]
+    for wi, w in enumerate(walls):
+        for k, p in enumerate(wpos):
+            ag.state.p_pos = p.copy()
+            f = world.get_wall_collision_force(ag, w)
+            if f is not None:
+                wforce[wi, k] = f
+    out = dict(pos=pos, done=np.array([a.done for a in world.agents]), forces=forces,
+               sizes=np.array([e.size for e in ents]), collide=np.array([e.collide for e in ents]),
+               movable=np.array([e.movable for e in ents]), mass=np.array([e.mass for e in ents]),
+               contact_force=world.contact_force, contact_margin=world.contact_margin,
+               wall_contact_force=world.wall_contact_force, wall_contact_margin=world.wall_contact_margin,
+               walls=np.array([[0 if w.orient == "H" else 1, w.axis_pos, w.endpoints[0], w.endpoints[1], w.width,
+                                float(w.hard)] for w in walls]), wall_pos=wpos, wall_force=wforce,
+               agent_size=ag.size)
+    path = os.path.join(HERE, "collision_forces.npz")
+    np.savez_compressed(path, **out)
+    print("wrote", path, "pairs with force:", int(np.isfinite(forces[..., 0, 0]).sum()),
+          "wall hits:", int(np.isfinite(wforce[..., 0]).sum()))
+
+
 def main(only=None):
     if not ref_harness.reference_available():
         raise SystemExit("reference not available here")
@@ -207,12 +271,16 @@ def main(only=None):
                          seed=23, ep=3, steps=200, value_stored=at_small, ttr_stored=ttr_small,
                          action_seed=9, runner_episodes=True, sep_curriculum=True),
     ]
+    if only == "collision":
+        record_collision_forces()
+        return
     if only == "sepcur":
         for f in sepcur:
             f()
         return
     for f in sepcur:
         f()
+    record_collision_forces()
     di_small = hj_tables.synthetic_di_stored((31, 31, 21, 21))
     at_small = hj_tables.synthetic_airtaxi_stored((25, 25, 24, 7, 7))
     ttr_small = hj_tables.synthetic_ttr((25, 25, 24, 7))

@@ -22,7 +22,10 @@ INFOKEYS = ("individual_reward", "min_relative_distance", "Dist_to_goal", "Time_
 
 
 def fixture_names():
-    return sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, "*.npz")))
+    """The rollout fixtures (each holds a "meta" record); collision_forces.npz is a function-level
+    fixture of its own (tests/test_collision_forces.py)."""
+    return sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, "*.npz"))
+                  if not os.path.basename(p).startswith("collision"))
 
 
 def load(name):

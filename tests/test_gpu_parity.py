@@ -549,3 +549,50 @@ def test_gpu_action_index_out_of_range_is_reported():
         env.check_actions()
     env.check_actions()                                   # the flag was cleared
     env.close()
+
+
+@pytest.mark.parametrize("kernel", ["wave", "block"])
+def test_gpu_collision_forces_reported_never_applied(kernel, monkeypatch):
+    """World.get_entity_collision_force (core.py:741-774) has no caller, so the step
+    must never apply contact forces. With lsm_config.collision_forces the kernel reports the
+    per-agent force (LSM_OUT_COLLISION_FORCE) -- compared with the oracle's restatement (itself
+    pinned to the reference's own function, tests/test_collision_forces.py) -- while every output
+    stays bit-identical to a run without the flag (the default)."""
+    if kernel == "block":
+        monkeypatch.setenv("LSM_KERNEL", "block")
+    meta = dict(dynamics_type="double_integrator", num_agents=8, num_landmarks=2, world_size=4,
+                episode_length=30, num_env_steps=30 * 4, n_rollout_threads=1, use_safety_filter=True,
+                use_masking=True, num_internal_step=1, seed=13, env_seed=13, collision_forces=True)
+    n = 12
+    on = _gpu_env(meta, n_envs=n, seed=13, collision_forces=True)
+    off = _gpu_env(meta, n_envs=n, seed=13)
+    assert off.t_cforce is None
+    ora = _oracle_for(meta, 13, n)
+    for e in (on, off, ora):
+        e.reset(4)
+    rng = np.random.default_rng(9)
+    strong = 0
+    for t in range(40):
+        if t in (5, 21):   # push agents 1 and 2 of some envs into contact (overlapping discs)
+            for k in (0, 3, 7):
+                oe = ora.envs[k]
+                st = oe.s.copy()
+                st[2, :2] = st[1, :2] + np.array([0.07, 0.02])
+                st[3, :2] = st[1, :2] + np.array([-0.04, 0.09])
+                for env in (on, off):
+                    env.set_agent_state(k, st)
+                oe.s[:] = st
+                oe.calculate_distances()
+        a = rng.integers(0, 25, (n, 8))
+        g_on, g_off, o = on.step(a, 4), off.step(a, 4), ora.step(a, 4)
+        for i in (0, 2, 3, 4, 5):
+            np.testing.assert_array_equal(g_on[i], g_off[i], err_msg="t=%d output %d" % (t, i))
+        np.testing.assert_array_equal(on.state().cpu().numpy(), off.state().cpu().numpy())
+        np.testing.assert_array_equal(g_on[5], o[5])
+        f = on.t_cforce.cpu().numpy()
+        want = np.stack([e.cforce for e in ora.envs])
+        np.testing.assert_allclose(f, want, rtol=1e-12, atol=1e-300, err_msg="t=%d" % t)
+        strong += int((np.abs(want) > 1e-3).any())
+    assert strong >= 2
+    on.close()
+    off.close()
