@@ -168,7 +168,8 @@ LSM_RK_HD double rk_gemv_col(const double* k, const double* w, int s) {
 //   * K[j][2..3] = a for every stage, so the velocity-component dot products depend on a only and
 //     are computed once per call instead of once per step;
 //   * the error factor min(10, 0.9 err^-1/5) is 10 without evaluating pow when err <= 1e-6
-//     (0.9 * (1e-6)^-0.2 = 14.2 > 10); err == 0 gives 10 as in scipy.
+//     (0.9 * (1e-6)^-0.2 = 14.2 > 10); err == 0 gives 10 as in scipy; after the step that
+//     reaches tb it is not evaluated at all (scipy computes the next step size, nothing reads it).
 // A rejected step (err >= 1) follows _step_impl: h *= max(0.2, 0.9 err^-1/5), factor <= 1 after.
 LSM_RK_HD int rk45_di(double* y, double a0, double a1, double tb) {
   const double rtol = 1e-3, atol = 1e-6;
@@ -238,13 +239,15 @@ LSM_RK_HD int rk45_di(double* y, double a0, double a1, double tb) {
       }
       const double en = rk_norm4(r4);
       if (en < 1) {
-        double fac = 10.0;           // MAX_FACTOR
-        if (en > 1e-6) {
-          const double q = 0.9 * glibc_pow(en, -1.0 / 5.0);
-          if (q < fac) fac = q;
+        if (t_new < tb) {            // the step size after the last step is never used
+          double fac = 10.0;         // MAX_FACTOR
+          if (en > 1e-6) {
+            const double q = 0.9 * glibc_pow(en, -1.0 / 5.0);
+            if (q < fac) fac = q;
+          }
+          if (rejected && fac > 1) fac = 1;
+          h_abs *= fac;
         }
-        if (rejected && fac > 1) fac = 1;
-        h_abs *= fac;
         t = t_new;
         y[0] = yn0; y[1] = yn1; y[2] = yn2; y[3] = yn3;
         v0 = yn2; v1 = yn3;

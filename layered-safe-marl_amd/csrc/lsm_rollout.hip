@@ -279,6 +279,21 @@ __device__ __forceinline__ void st_stream(GAS float* dst, float4 v) {
   else *(GAS f32x4*)dst = x;
 }
 
+// Synchronise the lanes of one env. An env of <= 64 lanes lives in one wave (the one-wave
+// kernels, and each wave of the team kernel, whose other waves hold other envs and must not be
+// waited for): LDS accesses of a wave complete in order, so a compiler fence + wave barrier
+// suffices. The workgroup-per-env kernel (LPE = BT) needs the workgroup barrier.
+template <int LPE>
+__device__ __forceinline__ void esync() {
+  if (LPE > 64) {
+    __syncthreads();
+  } else {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+}
+
 // all() over the LPE-lane group of the calling lane (one env)
 template <int LPE>
 __device__ __forceinline__ bool group_all(bool v) {
@@ -467,13 +482,7 @@ struct WaveRng {
   uint32_t* key;
   int pos;
   __device__ __forceinline__ void sync() {
-    if (WSYNC) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    } else {
-      __syncthreads();
-    }
+    esync<(WSYNC ? WAVE : LPE)>();
   }
   __device__ __forceinline__ void gen() {
     // chunks of C <= 64 lanes: phase B's element i reads the NEW key[i - 227], so a chunk
@@ -841,7 +850,7 @@ __device__ __forceinline__ double magnetic_penalty_wave(const KParams& P, Lds& S
   }
   part[lane] = m0;
   part[LPE + lane] = m1;
-  __syncthreads();
+  esync<LPE>();
   double pen = 0.0;
   if (lane < N) {
     const int i = lane;
@@ -876,7 +885,7 @@ __device__ __forceinline__ double magnetic_penalty_wave(const KParams& P, Lds& S
       pen = err * (1 - ar) + dist * ar;
     }
   }
-  __syncthreads();
+  esync<LPE>();
   return pen;
 }
 
@@ -942,15 +951,29 @@ __device__ __forceinline__ void filter_ego(const KParams& P, Lds& S, int i, uint
 // optimal control (V < eps_hj) or the closed-form CBF-QP, clips (safety_filter.py:264-308,
 // 395-433).
 template <int DYN, int NT>
+__device__ __forceinline__ void filter_qp(const KParams& P, const Lds& S, int i, int jv, float vmin,
+                                          const double* rel, const float* g, uint8_t& filtered, double& u0,
+                                          double& u1);
+
+template <int DYN, int NT>
 __device__ __forceinline__ void filter_apply(const KParams& P, const Lds& S, int i, int jv, float vmin,
                                              uint8_t& filtered, double& u0, double& u1) {
   LSM_DIMS;
-  const int ND = (DYN == 0) ? 4 : 5;
   double rel[5];
   rel_state<DYN>(S, N, i, jv, rel);
-  double uref[4] = {S.raw[i], S.raw[N + i], S.raw[jv], S.raw[N + jv]};
   float g[5];
   if (DYN == 0) interp_grad<4>(P.val, rel, g); else interp_grad<5>(P.val, rel, g);
+  filter_qp<DYN, NT>(P, S, i, jv, vmin, rel, g, filtered, u0, u1);
+}
+
+// The filter's control once the HJ gradient g at the relative state rel is known.
+template <int DYN, int NT>
+__device__ __forceinline__ void filter_qp(const KParams& P, const Lds& S, int i, int jv, float vmin,
+                                          const double* rel, const float* g, uint8_t& filtered, double& u0,
+                                          double& u1) {
+  LSM_DIMS;
+  const int ND = (DYN == 0) ? 4 : 5;
+  double uref[4] = {S.raw[i], S.raw[N + i], S.raw[jv], S.raw[N + jv]};
   const float V = vmin;
   double u[4];
   bool alias = false;   // infeasible QP returns u_ref itself (safety_filter.py:304-305,373-375)
@@ -1166,14 +1189,16 @@ __device__ __forceinline__ void build_rows_di(const KParams& P, Lds& S) {
   const int lane = threadIdx.x & (LPE - 1);
   constexpr int DYN = 0;
   LSM_DIMS;
+  const int32_t* dpost = S.dpost;
+  const int32_t* rpost = S.rpost;
   for (int t = lane; t < 2 * N + NL; t += LPE) {
     double* r = S.feat + (size_t)t * F;
     if (t < 2 * N) {
       const bool post = t >= N;
       const int k = post ? t - N : t;
-      double vx, vy;
-      agent_vel<0>(S, N, k, post, vx, vy);
-      const int gi = goal_index(post ? S.rpost[k] : S.rpre[k], k, N, NL);
+      const bool frozen = post && dpost[k];
+      const double vx = frozen ? 0.0 : S.ps[2 * N + k], vy = frozen ? 0.0 : S.ps[3 * N + k];
+      const int gi = goal_index(post ? rpost[k] : S.rpre[k], k, N, NL);
       r[0] = S.ps[k]; r[1] = S.ps[N + k]; r[2] = vx; r[3] = vy;
       r[4] = S.lm[gi]; r[5] = S.lm[NL + gi];
       r[6] = S.lmsc[gi]; r[7] = S.lmsc[NL + gi]; r[8] = S.lm[3 * NL + gi]; r[9] = 0.0;
@@ -1186,8 +1211,8 @@ __device__ __forceinline__ void build_rows_di(const KParams& P, Lds& S) {
   }
   if (lane < N) {
     const int e = lane;
-    double vx, vy;
-    agent_vel<0>(S, N, e, true, vx, vy);
+    const bool frozen = dpost[e] != 0;
+    const double vx = frozen ? 0.0 : S.ps[2 * N + e], vy = frozen ? 0.0 : S.ps[3 * N + e];
     double* o = S.egooff + e * F;
     o[0] = S.ps[e]; o[1] = S.ps[N + e]; o[2] = vx; o[3] = vy; o[4] = S.ps[e]; o[5] = S.ps[N + e];
     o[6] = 0.0; o[7] = 0.0; o[8] = 0.0; o[9] = 0.0;
@@ -1248,7 +1273,7 @@ __device__ __forceinline__ void emit_graph(const KParams& P, Lds& S, int env, bo
   const int lane = threadIdx.x & (LPE - 1);
   LSM_DIMS;
   if (DYN == 0) build_rows_di<LPE, NT>(P, S); else trig_table_at<LPE, NT>(P, S);
-  __syncthreads();
+  esync<LPE>();
   // No agent changed done / reached status this step (the common case): every ego then has
   // the same disconnect mask and the same (pre == post) entity rows, so each lane computes
   // its output words once and stores them for all N egos.
@@ -1314,6 +1339,38 @@ __device__ __forceinline__ void emit_graph(const KParams& P, Lds& S, int env, bo
 
 // node_obs [N][E][F] of one env (DI rows / airtaxi trig table already in LDS). `uni`: no
 // agent changed status this step, so every ego sees the post rows.
+// DI node_obs of egos [e0, e1) when no agent changed status (E * F % 4 == 0): lane owns float4 t
+// of every ego block, entity rows read once, ego offset per ego.
+template <int LPE, int NT>
+__device__ __forceinline__ void emit_nodes_uniform_di(const KParams& P, const Lds& S, int env, int e0, int e1) {
+  const int lane = threadIdx.x & (LPE - 1);
+  constexpr int DYN = 0;
+  LSM_DIMS;
+  GAS float* node_out = gptr(P.o.node) + (size_t)env * N * E * F;
+  const int EF4 = E * F / 4;
+  for (int t = lane; t < EF4; t += LPE) {
+    int k = qdiv<NT>(4 * t, F, P.m_F);
+    int q = 4 * t - k * F;
+    double fv[4];
+    int qq[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      fv[c] = S.feat[(N + k) * F + q];   // post rows == pre rows here; landmarks at N + k
+      qq[c] = q;
+      if (++q == F) { q = 0; ++k; }
+    }
+#ifdef LSM_STAMPS
+    if (P.diag & 1) continue;
+#endif
+    for (int e = e0; e < e1; ++e) {
+      const double* o = S.egooff + e * F;
+      st_stream<(NT >= 16)>(node_out + (size_t)e * E * F + 4 * t,
+          make_float4((float)(fv[0] - o[qq[0]]), (float)(fv[1] - o[qq[1]]), (float)(fv[2] - o[qq[2]]),
+                      (float)(fv[3] - o[qq[3]])));
+    }
+  }
+}
+
 template <int DYN, int LPE, int NT>
 __device__ __forceinline__ void emit_nodes(const KParams& P, Lds& S, int env, bool uni) {
   const int lane = threadIdx.x & (LPE - 1);
@@ -1321,29 +1378,7 @@ __device__ __forceinline__ void emit_nodes(const KParams& P, Lds& S, int env, bo
   const int npairs = N * E, ntot = npairs * F;
   GAS float* node_out = gptr(P.o.node) + (size_t)env * ntot;
   if (DYN == 0 && ((E * F) & 3) == 0 && uni) {
-    // lane owns float4 t of every ego block: entity rows read once, ego offset per ego
-    const int EF4 = E * F / 4;
-    for (int t = lane; t < EF4; t += LPE) {
-      int k = qdiv<NT>(4 * t, F, P.m_F);
-      int q = 4 * t - k * F;
-      double fv[4];
-      int qq[4];
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        fv[c] = S.feat[(N + k) * F + q];   // post rows == pre rows here; landmarks at N + k
-        qq[c] = q;
-        if (++q == F) { q = 0; ++k; }
-      }
-#ifdef LSM_STAMPS
-      if (P.diag & 1) continue;
-#endif
-      for (int e = 0; e < N; ++e) {
-        const double* o = S.egooff + e * F;
-        st_stream<(NT >= 16)>(node_out + (size_t)e * E * F + 4 * t,
-            make_float4((float)(fv[0] - o[qq[0]]), (float)(fv[1] - o[qq[1]]), (float)(fv[2] - o[qq[2]]),
-                        (float)(fv[3] - o[qq[3]])));
-      }
-    }
+    emit_nodes_uniform_di<LPE, NT>(P, S, env, 0, N);
     return;
   }
   if (DYN == 0 && ((E * F) & 3) == 0) {
@@ -1367,7 +1402,7 @@ __device__ __forceinline__ void emit_nodes(const KParams& P, Lds& S, int env, bo
     }
     return;
   }
-  __syncthreads();   // fval dead from here: node staging reuses U1
+  esync<LPE>();   // fval dead from here: node staging reuses U1
   const bool nvec = (ntot & 3) == 0;
   for (int b0 = 0; b0 < npairs; b0 += LPE) {
     const int p = b0 + lane;
@@ -1388,7 +1423,7 @@ __device__ __forceinline__ void emit_nodes(const KParams& P, Lds& S, int env, bo
         for (int q = 0; q < 11; ++q) st[q] = f[q];
       }
     }
-    __syncthreads();
+    esync<LPE>();
     const int cnt = min(LPE, npairs - b0) * F;
     GAS float* dst = node_out + (size_t)b0 * F;
     if (nvec && (cnt & 3) == 0) {
@@ -1396,7 +1431,7 @@ __device__ __forceinline__ void emit_nodes(const KParams& P, Lds& S, int env, bo
     } else {
       for (int q = lane; q < cnt; q += LPE) dst[q] = S.stage[q];
     }
-    __syncthreads();
+    esync<LPE>();
   }
 }
 
@@ -1450,7 +1485,7 @@ __device__ __forceinline__ void compute_dist(const KParams& P, Lds& S, const uin
     S.fval[k * E + k] = 0.0f;
     if (k < N) { S.aa[k * N + k] = 0.0; S.aa2[k * N + k] = 0.0; }
   }
-  __syncthreads();
+  esync<LPE>();
 }
 
 template <int DYN, int NT>
@@ -1599,7 +1634,7 @@ __device__ __forceinline__ void reset_core(const KParams& P, Lds& S, int env, co
       gptr(P.o.ep_info)[(size_t)env * 8 + k] = outv[k];
     }
   }
-  __syncthreads();
+  esync<LPE>();
   for (int k = lane; k < NCUR; k += LPE) S.cur[k] = cur_new[k];
   if (lane == 0 && P.use_filter_arg) {
     // update_curriculum -> world.update_safety_filter_separation_distance -> HjDataHandle.
@@ -1617,7 +1652,7 @@ __device__ __forceinline__ void reset_core(const KParams& P, Lds& S, int env, co
   }
   const GAS uint32_t* mtg = gptr(P.s.mt) + (size_t)env * MT_WORDS;
   for (int k = lane; k < MT_WORDS; k += LPE) S.mt[k] = mtg[k];
-  __syncthreads();
+  esync<LPE>();
   ScenarioParams sp;
   sp.dyn = DYN; sp.N = N; sp.L = L; sp.world_size = P.world_size; sp.coordination_range = P.coord_range;
   sp.goal_speed_min = P.gs_min; sp.goal_speed_max = P.gs_max;
@@ -1632,16 +1667,16 @@ __device__ __forceinline__ void reset_core(const KParams& P, Lds& S, int env, co
       random_scenario(rng, sp, S.ps, S.lm, S.scen);
       if (lane == 0) S.mt[MT_N] = (uint32_t)rng.pos;
     }
-    __syncthreads();
+    esync<LPE>();
   } else {
     WaveRng<LPE> rng;
     rng.key = S.mt;
     rng.pos = (int)S.mt[MT_N];
     // every lane runs the identical draw sequence and stores the identical values
     random_scenario(rng, sp, S.ps, S.lm, S.scen);
-    __syncthreads();
+    esync<LPE>();
     if (lane == 0) S.mt[MT_N] = (uint32_t)rng.pos;
-    __syncthreads();
+    esync<LPE>();
   }
   GAS uint32_t* mtw = gptr(P.s.mt) + (size_t)env * MT_WORDS;
   for (int k = lane; k < MT_WORDS; k += LPE) mtw[k] = S.mt[k];
@@ -1658,7 +1693,7 @@ __device__ __forceinline__ void reset_core(const KParams& P, Lds& S, int env, co
     S.gmt[k] = plain_norm2(S.ps[k] - S.lm[k], S.ps[N + k] - S.lm[NL + k]) / P.max_speed;
   }
   if (lane == 0) { S.step[0] = 0; S.step[1] = 0; }
-  __syncthreads();   // MT words read out of U1 before compute_dist overwrites it
+  esync<LPE>();   // MT words read out of U1 before compute_dist overwrites it
 }
 
 template <int DYN, int LPE, int NT>
@@ -1704,7 +1739,7 @@ __device__ __forceinline__ void store_state(const KParams& P, Lds& S, const unsi
     S.ps[k] = v;
     if (P.o.state) gptr(P.o.state)[((size_t)env * N + j) * 4 + c] = v;
   }
-  __syncthreads();
+  esync<LPE>();
   rec_copy<LPE>((const f32x4*)lbase, (GAS f32x4*)gptr(P.s.rec) + (size_t)env * P.s.rec_stride16, full ? P.s.rec16 : P.s.hot16);
 }
 
@@ -1916,8 +1951,8 @@ __device__ __forceinline__ void info_agent(const KParams& P, Lds& S, int i, int 
 
 // agent i's info row (LSM_INFO_FIELDS doubles at `inf`), after every agent's info_agent:
 // Distance / Time mean and std over the agents under the sequential snapshot rule.
-template <int NT>
-__device__ __forceinline__ void info_row(const KParams& P, const Lds& S, int i, double rew, double* inf) {
+template <int NT, class DP>
+__device__ __forceinline__ void info_row(const KParams& P, const Lds& S, int i, double rew, DP inf) {
   constexpr int DYN = 0;
   LSM_DIMS;
   struct Snap {
@@ -1966,6 +2001,95 @@ __device__ __forceinline__ void stats_agent(const KParams& P, Lds& S, int N, int
   }
 }
 
+// The end-of-step episode statistics of agent i (environment.py:1004-1022) over the agents its
+// final disconnect mask S.emask[i] keeps; `departed` is always True in the training scenario.
+template <int DYN>
+__device__ __forceinline__ void episode_stats(const KParams& P, Lds& S, int N, int i) {
+  if (!S.dpost[i]) {
+    const uint64_t m = S.emask[i];
+    int cnt = 0, neng = 0;
+    double mn = INFINITY;
+    for (int j = 0; j < N; ++j) {
+      if (((m >> i) | (m >> j)) & 1ull) continue;
+      const double d = S.aa[i * N + j];
+      if (!(d < P.coord_range && d > 0)) continue;
+      cnt++;
+      if (d < P.world_eng) neng++;
+      mn = (d < mn) ? d : mn;
+    }
+    stats_agent<DYN>(P, S, N, i, cnt, neng, mn);
+  }
+  if (S.dpost[i]) S.stats[2 * N + i] = 1;
+}
+
+// min relative distance of agent i over the other active agents (core.py:696-709)
+__device__ __forceinline__ void min_relative(Lds& S, int N, int i) {
+  double m = INFINITY;
+  if (!S.dpre[i]) {
+    for (int j = 0; j < N; ++j) {
+      if (j == i || S.dpre[j]) continue;
+      const double d = S.aa2[i * N + j];
+      m = (d < m) ? d : m;
+    }
+  }
+  S.minrel[i] = m;
+}
+
+// other agents within the collision distance of agent i (is_collision, navigation_graph_safe.py:497-501)
+__device__ __forceinline__ int collision_count(const Lds& S, int N, int i) {
+  int cc = 0;
+  for (int a = 0; a < N; ++a)
+    if (a != i && S.aa2[i * N + a] < 1.05 * (0.05 + 0.05)) cc++;
+  return cc;
+}
+
+// This step's Discrete(25) action index of agent `i` of env `env` (index, or the argmax of a
+// one-hot row as the reference's np.argmax decode, environment.py:386-410).
+__device__ __forceinline__ int read_action(const KStep& K, int env, int N, int i) {
+  const size_t base = (size_t)env * N + i;
+  int ai = 0;
+  if (K.action_kind == LSM_ACTIONS_INDEX_I32) {
+    ai = ((const GAS int32_t*)gptr(K.actions))[base];
+  } else if (K.action_kind == LSM_ACTIONS_ONEHOT_F32) {
+    const GAS float* a = (const GAS float*)gptr(K.actions) + base * 25;
+    float best = a[0];
+    for (int q = 1; q < 25; ++q) if (a[q] > best) { best = a[q]; ai = q; }
+  } else {
+    const GAS double* a = (const GAS double*)gptr(K.actions) + base * 25;
+    double best = a[0];
+    for (int q = 1; q < 25; ++q) if (a[q] > best) { best = a[q]; ai = q; }
+  }
+  return ai;
+}
+
+// decode into the env's raw action rows; an index outside Discrete(25) is an error of the
+// caller (the reference's one-hot decode has no such input): flagged for lsm_action_errors(),
+// and the launch kept in bounds
+__device__ __forceinline__ void decode_action(const KParams& P, Lds& S, int N, int i, int ai) {
+  if (ai < 0 || ai > 24) *gptr(P.action_err) = 1;
+  const int a = ai < 0 ? 0 : (ai > 24 ? 24 : ai);
+  const int xi = a / 5, yi = a - xi * 5;
+  S.raw[i] = P.act0[xi];
+  S.raw[N + i] = P.act1[yi];
+}
+
+// Safety filter of agent i once the pair scratch is filled (core.py:648-677): the filtered
+// action, flag, deconflicting index and action difference.
+template <int DYN, int NT>
+__device__ __forceinline__ void filter_agent(const KParams& P, Lds& S, int N, int i, bool filter_on) {
+  double u0 = S.raw[i], u1 = S.raw[N + i];
+  if (filter_on) {
+    uint8_t fl = 0;
+    int dec = -1;
+    if (!S.dpre[i]) filter_ego<DYN, NT>(P, S, i, fl, dec, u0, u1);
+    S.sfilt[i] = fl;
+    S.decon[i] = dec;
+  }
+  S.safe[i] = u0;
+  S.safe[N + i] = u1;
+  S.adiff[i] = blas_norm2(S.raw[i] - u0, S.raw[N + i] - u1);
+}
+
 // Double integrator: 4 waves per SIMD (<= 128 VGPRs): config 3 is exactly 4096 one-wave envs =
 // 4 per SIMD, and at 134 VGPRs the 4th wave of every SIMD ran after the others (53 vs 41 us per
 // step, measured). Airtaxi keeps 2 (~176 VGPRs; a 128 cap spills 200-350 B per lane).
@@ -1994,20 +2118,7 @@ __global__ __launch_bounds__(64, DYN == 0 ? (LPE == 64 ? 4 : 2) : LSM_WAVES_PER_
 
   // ---- 0. the env's record HBM -> LDS (one round trip) + this step's actions ------------
   int ai = 0;
-  if (K.mode == 0 && lane < N) {
-    const size_t base = (size_t)env * N + lane;
-    if (K.action_kind == LSM_ACTIONS_INDEX_I32) {
-      ai = ((const GAS int32_t*)gptr(K.actions))[base];
-    } else if (K.action_kind == LSM_ACTIONS_ONEHOT_F32) {
-      const GAS float* a = (const GAS float*)gptr(K.actions) + base * 25;
-      float best = a[0];
-      for (int q = 1; q < 25; ++q) if (a[q] > best) { best = a[q]; ai = q; }
-    } else {
-      const GAS double* a = (const GAS double*)gptr(K.actions) + base * 25;
-      double best = a[0];
-      for (int q = 1; q < 25; ++q) if (a[q] > best) { best = a[q]; ai = q; }
-    }
-  }
+  if (K.mode == 0 && lane < N) ai = read_action(K, env, N, lane);
   // this lane's E x E pair words (compute_dist), loaded in the same round trip as the record
   constexpr bool PRE = NT != 0 && NT <= 8;   // <= 5 registers per lane
   constexpr int NPI = PRE ? ((NT * (NT - 1) / 2 + NT * 2 * NT) + LPE - 1) / LPE : 1;
@@ -2064,15 +2175,7 @@ __global__ __launch_bounds__(64, DYN == 0 ? (LPE == 64 ? 4 : 2) : LSM_WAVES_PER_
   }
 
   // ---- 2. decode actions ----------------------------------------------------------
-  if (lane < N) {
-    // an index outside Discrete(25) is an error of the caller (the reference's one-hot decode has
-    // no such input): flag it for lsm_action_errors(), and keep the launch in bounds
-    if (ai < 0 || ai > 24) *gptr(P.action_err) = 1;
-    int a = ai < 0 ? 0 : (ai > 24 ? 24 : ai);
-    const int xi = a / 5, yi = a - xi * 5;
-    S.raw[lane] = P.act0[xi];
-    S.raw[N + lane] = P.act1[yi];
-  }
+  if (lane < N) decode_action(P, S, N, lane, ai);
   __syncthreads();
   STAMP(2);
 
@@ -2101,20 +2204,7 @@ __global__ __launch_bounds__(64, DYN == 0 ? (LPE == 64 ? 4 : 2) : LSM_WAVES_PER_
     __syncthreads();
   }
   STAMP(3);
-  if (lane < N) {
-    const int i = lane;
-    double u0 = S.raw[i], u1 = S.raw[N + i];
-    if (filter_on) {
-      uint8_t fl = 0;
-      int dec = -1;
-      if (!S.dpre[i]) filter_ego<DYN, NT>(P, S, i, fl, dec, u0, u1);
-      S.sfilt[i] = fl;
-      S.decon[i] = dec;
-    }
-    S.safe[i] = u0;
-    S.safe[N + i] = u1;
-    S.adiff[i] = blas_norm2(S.raw[i] - u0, S.raw[N + i] - u1);
-  }
+  if (lane < N) filter_agent<DYN, NT>(P, S, N, lane, filter_on);
   __syncthreads();
   STAMP(4);
 
@@ -2132,18 +2222,7 @@ __global__ __launch_bounds__(64, DYN == 0 ? (LPE == 64 ? 4 : 2) : LSM_WAVES_PER_
     cf[0] = fx;
     cf[1] = fy;
   }
-  if (lane < N) {
-    const int i = lane;
-    double m = INFINITY;
-    if (!S.dpre[i]) {
-      for (int j = 0; j < N; ++j) {
-        if (j == i || S.dpre[j]) continue;
-        const double d = S.aa2[i * N + j];
-        m = (d < m) ? d : m;
-      }
-    }
-    S.minrel[i] = m;
-  }
+  if (lane < N) min_relative(S, N, lane);
   // Speculative adjacency: unless an agent changes done / reached status below (rare), every
   // ego's mask is the pre-update mask, so the adjacency can be stored now, in four chunks of
   // egos placed between the remaining phases: the stores drain while the wave computes
@@ -2165,12 +2244,7 @@ __global__ __launch_bounds__(64, DYN == 0 ? (LPE == 64 ? 4 : 2) : LSM_WAVES_PER_
   STAMP(7);
 
   // ---- 7/8. info_callback numbers -----------------------------------------------------
-  if (lane < N) {
-    int cc = 0;
-    for (int a = 0; a < N; ++a)
-      if (a != lane && S.aa2[lane * N + a] < 1.05 * (0.05 + 0.05)) cc++;
-    info_agent<DYN, NT>(P, S, lane, cstep, at, cc);
-  }
+  if (lane < N) info_agent<DYN, NT>(P, S, lane, cstep, at, collision_count(S, N, lane));
   __syncthreads();
   if (lane < N) info_row<NT>(P, S, lane, rew, S.dpair + lane * LSM_INFO_FIELDS);   // staged in U2
   __syncthreads();
@@ -2183,21 +2257,7 @@ __global__ __launch_bounds__(64, DYN == 0 ? (LPE == 64 ? 4 : 2) : LSM_WAVES_PER_
   bool my_done = true;
   if (lane < N) {
     const int i = lane;
-    if (!S.dpost[i]) {  // departed is always True in the training scenario
-      const uint64_t m = S.emask[i];
-      int cnt = 0, neng = 0;
-      double mn = INFINITY;
-      for (int j = 0; j < N; ++j) {
-        if (((m >> i) | (m >> j)) & 1ull) continue;
-        const double d = S.aa[i * N + j];
-        if (!(d < P.coord_range && d > 0)) continue;
-        cnt++;
-        if (d < P.world_eng) neng++;
-        mn = (d < mn) ? d : mn;
-      }
-      stats_agent<DYN>(P, S, N, i, cnt, neng, mn);
-    }
-    if (S.dpost[i]) S.stats[2 * N + i] = 1;
+    episode_stats<DYN>(P, S, N, i);
     my_done = S.dpost[i] || cstep >= P.episode_length;
     gptr(P.o.dones)[(size_t)env * N + i] = my_done ? 1 : 0;
   }
@@ -2227,6 +2287,7 @@ __global__ __launch_bounds__(64, DYN == 0 ? (LPE == 64 ? 4 : 2) : LSM_WAVES_PER_
 }
 
 #include "lsm_block.h"
+#include "lsm_team.h"
 
 // A new value table (a new HjDataHandle): every env's separation chain starts empty.
 __global__ void sep_clear_kernel(float4* rec, uint32_t rec_stride16, int n_envs, uint32_t sep_off) {
@@ -2287,6 +2348,7 @@ struct lsm_env {
   int lpe;   // lanes per env
   bool block;   // workgroup-per-env kernel (N > 32 or E > 64, or LSM_KERNEL=block)
   bool generic_only;   // LSM_GENERIC=1: never use the compile-time-N kernels (tests): 64 (one env per wave), 32 or 16 (2 or 4 envs per wave)
+  int team;   // envs per workgroup of the team kernel (lsm_team.h); 0 = rollout_kernel
 };
 
 static int fail(lsm_env* e, const std::string& msg) {
@@ -2467,6 +2529,20 @@ int lsm_create(const lsm_config* cfg, lsm_env** out) {
   if (const char* v = getenv("LSM_LPE")) e->lpe = atoi(v);
   e->generic_only = getenv("LSM_GENERIC") && atoi(getenv("LSM_GENERIC")) != 0;
   if (e->block) e->lpe = 64;   // LSM_LPE applies to the one-wave kernel only
+  // Team kernel (lsm_team.h) for the compile-time-N BASELINE agent counts: G envs per
+  // workgroup share one wave for their per-agent phases. LSM_TEAM=0 selects rollout_kernel,
+  // LSM_TEAM=G another instantiated G.
+  e->team = 0;
+  if (!e->block && e->lpe == 64 && L == 2 && !e->generic_only) {
+    if (cfg->dynamics == LSM_DOUBLE_INTEGRATOR && N == 8) e->team = 4;   // measured: 4 < 8 < 2 (us/step)
+    if (cfg->dynamics == LSM_AIRTAXI && N == 16) e->team = 2;
+    if (const char* v = getenv("LSM_TEAM")) {
+      const int g = atoi(v);
+      if (g == 0) e->team = 0;
+      else if (e->team && g * N <= 64 && (g == 2 || g == 4 || g == 8)) e->team = g;
+      else if (e->team) return fail(e, "LSM_TEAM must be 0, 2, 4 or 8 with LSM_TEAM * num_agents <= 64");
+    }
+  }
   if (!(e->lpe == 16 || e->lpe == 32 || e->lpe == 64) || e->lpe < (e->block ? 1 : N))
     return fail(e, "LSM_LPE must be 16, 32 or 64 and >= num_agents");
   HIPCHK(e, hipGetDevice(&e->device));
@@ -2766,6 +2842,21 @@ static void launch_t(lsm_env* e, const KStep& L, size_t env_lds, hipStream_t st)
                      active_params(e), L);
 }
 
+extern "C++" template <int DYN, int NT, int G>
+static int launch_team_t(lsm_env* e, const KStep& L, size_t env_bytes, hipStream_t st) {
+  static bool attr = false;   // LDS above the 64 KB default needs an explicit opt-in
+  const size_t lds = env_bytes * G;
+  if (!attr && lds > 65536) {
+    HIPCHK(e, hipFuncSetAttribute((const void*)rollout_team_kernel<DYN, NT, G>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    attr = true;
+  }
+  const int blocks = (e->cfg.num_envs + G - 1) / G;
+  hipLaunchKernelGGL((rollout_team_kernel<DYN, NT, G>), dim3(blocks), dim3(WAVE * G), lds, st,
+                     active_params(e), L);
+  return 0;
+}
+
 extern "C++" template <int DYN, int NT>
 static int launch_block_t(lsm_env* e, const KStep& L, size_t env_lds, hipStream_t st) {
   static bool attr = false;   // LDS above the 64 KB default needs an explicit opt-in
@@ -2780,8 +2871,10 @@ static int launch_block_t(lsm_env* e, const KStep& L, size_t env_lds, hipStream_
 }
 
 static int launch(lsm_env* e, KStep& L, hipStream_t st) {
-  const size_t env_lds = lds_plan(e->N, e->NL, e->E, e->F, e->block).bytes;
-  if (e->block ? env_lds > 160 * 1024 : env_lds * (WAVE / e->lpe) > 65536)
+  size_t env_lds = lds_plan(e->N, e->NL, e->E, e->F, e->block).bytes;
+  if (e->team) env_lds = team_env_bytes(env_lds, e->N);
+  if (e->block ? env_lds > 160 * 1024
+               : (e->team ? env_lds * e->team > 160 * 1024 : env_lds * (WAVE / e->lpe) > 65536))
     return fail(e, "LDS footprint too large");
   if (e->params_dirty) {   // outputs / tables changed: refresh the device copy (stream-ordered)
     KParams P;
@@ -2814,6 +2907,20 @@ static int launch(lsm_env* e, KStep& L, hipStream_t st) {
     int rc;
     if (di) rc = spec64 ? launch_block_t<0, 64>(e, L, env_lds, st) : launch_block_t<0, 0>(e, L, env_lds, st);
     else rc = spec64 ? launch_block_t<1, 64>(e, L, env_lds, st) : launch_block_t<1, 0>(e, L, env_lds, st);
+    if (rc) return rc;
+    HIPCHK(e, hipGetLastError());
+    return 0;
+  }
+  if (e->team) {
+    int rc = 1;
+    if (di) {
+      if (e->team == 8) rc = launch_team_t<0, 8, 8>(e, L, env_lds, st);
+      else if (e->team == 4) rc = launch_team_t<0, 8, 4>(e, L, env_lds, st);
+      else rc = launch_team_t<0, 8, 2>(e, L, env_lds, st);
+    } else {
+      if (e->team == 4) rc = launch_team_t<1, 16, 4>(e, L, env_lds, st);
+      else rc = launch_team_t<1, 16, 2>(e, L, env_lds, st);
+    }
     if (rc) return rc;
     HIPCHK(e, hipGetLastError());
     return 0;

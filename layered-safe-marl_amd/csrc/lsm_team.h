@@ -1,0 +1,258 @@
+// lsm_team.h -- the "team" one-wave kernel: G envs per workgroup, one wave per env for the
+// env-wide phases, ONE wave for the per-agent phases of all G envs.
+//
+// Included by lsm_rollout.hip after rollout_kernel (same helpers, same arithmetic, same
+// outputs). Why: in rollout_kernel the per-agent float64 phases -- the filter's argmin and QP,
+// RK45, obs / reward / goal update, info, episode statistics -- run on N of a wave's 64 lanes
+// (8 of 64 at config 3), yet every one of those instructions costs a full wave issue slot. At
+// 4096 envs the SIMDs are issue-bound (4 waves each, measured), so the idle lanes are the cost.
+// Here the G = 64 / N envs of a workgroup put their agents side by side in one wave -- lane
+// g * N + i is agent i of env g -- so that work is issued once for G envs, while the pair,
+// distance and output phases keep one 64-lane wave per env. The other waves wait at the
+// workgroup barrier (no issue) or, during the reward / info phase, store their adjacency.
+//
+// Phases (W = workgroup barrier; every wave reaches each W the same number of times):
+//   A  (each env's wave)   record HBM -> LDS, actions, update_graph edges, decode, HJ pair lookups
+//   W  B (agent wave 0)    filter per agent, integrate                  (core.py:648-687)
+//   W  C (each env's wave) E x E distances, contact forces, magnetic field sums (filter off)
+//   W  D (agent wave 1%G)  min relative distance, obs / reward / goal update, disconnect masks,
+//                          info, episode stats;   other waves: speculative adjacency stores
+//   W  E (each env's wave) info rows out, dones / masks, then the auto-reset or the graph outputs
+//
+// LDS: the workgroup holds G env blocks of `lds_env_bytes`, padded (team_env_bytes) so that the
+// agent wave's lanes of different envs fall on different banks.
+#pragma once
+// (included inside namespace lsm)
+
+// Env block stride for the team kernel: a multiple of 8 NT bytes with an odd quotient, so the
+// 8-B per-agent fields of envs g = 0, 1, ... of one 32-lane ds_read_b64 group (256-B bank row)
+// start on distinct bank offsets.
+__host__ __device__ inline size_t team_env_bytes(size_t bytes, int N) {
+  const size_t u = 8 * (size_t)N;
+  size_t q = (bytes + u - 1) / u;
+  if ((q & 1) == 0) ++q;
+  return q * u;
+}
+
+// Team kernels target 4 waves / SIMD for the double integrator (<= 128 VGPRs, as rollout_kernel)
+// and 2 for airtaxi.
+// Diagnostic builds (-DLSM_STAMPS, lsm.diag_stamps --team): s_memtime of each env's wave at the
+// phase boundaries: 0 start, 6/7/8 own work of phases A / C / D done, 1-4 after barriers 1-4,
+// 5 end; 13/14 realtime start / end; 15 HW_ID | XCC_ID << 32. Never in the product library.
+#ifdef LSM_STAMPS
+#define TSTAMP(k)                                                                                  \
+  do {                                                                                             \
+    if (lane == 0 && live && gptr(P.stamps)) gptr(P.stamps)[(size_t)env * 16 + (k)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#define TRTSTAMP(k)                                                                                \
+  do {                                                                                             \
+    if (lane == 0 && live && gptr(P.stamps)) gptr(P.stamps)[(size_t)env * 16 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define TSTAMP(k) do { } while (0)
+#define TRTSTAMP(k) do { } while (0)
+#endif
+
+template <int DYN, int NT, int G>
+__global__ __launch_bounds__(64 * G) __attribute__((amdgpu_waves_per_eu(DYN == 0 ? 4 : 2)))
+void rollout_team_kernel(const KParams* __restrict__ Pp, const KStep K) {
+  static_assert(NT > 0 && G >= 2 && G * NT <= 64, "team: G envs x NT agents in one wave");
+  constexpr int LPE = 64;
+  const KParams& P = *Pp;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int w = (int)threadIdx.x >> 6;        // this wave's env slot
+  const int lane = (int)threadIdx.x & 63;
+  const int env0 = (int)blockIdx.x * G;
+  const int env = env0 + w;
+  const bool live = env < P.n_envs;           // wave-uniform
+  LSM_DIMS;
+  const uint32_t B = P.lds_env_bytes;
+  unsigned char* lbase = smem + (size_t)w * B;
+  Lds S = carve(lbase, N, NL, E, F);
+  // agent view: lane = g * NT + i
+  const int ag = lane / NT;
+  const int ai = lane - ag * NT;
+  const bool alane = ag < G && env0 + ag < P.n_envs;
+  const int aslot = ag < G ? ag : 0;
+  const int aenv = env0 + aslot;
+  Lds A = carve(smem + (size_t)aslot * B, N, NL, E, F);
+  constexpr int WB = 0, WD = 1 % G;           // agent-phase waves (different SIMDs)
+  TRTSTAMP(13);
+  TSTAMP(0);
+#ifdef LSM_STAMPS
+  if (lane == 0 && live && gptr(P.stamps))
+    gptr(P.stamps)[(size_t)env * 16 + 15] = (unsigned long long)__builtin_amdgcn_s_getreg(63492) |
+                                          ((unsigned long long)__builtin_amdgcn_s_getreg(6164) << 32);
+#endif
+
+  // ---- A. record HBM -> LDS, actions, edges, decode, pair lookups --------------------------
+  constexpr bool PRE = NT <= 8;
+  constexpr int NPI = PRE ? ((NT * (NT - 1) / 2 + NT * 2 * NT) + LPE - 1) / LPE : 1;
+  uint32_t prw[NPI];
+  int act = 0;
+  int cstep = 0;
+  bool filter_on = false;
+  if (live) {
+    if (K.mode == 0 && lane < N) act = read_action(K, env, N, lane);
+    if (PRE) {
+#pragma unroll
+      for (int k = 0; k < NPI; ++k) {
+        const int t = lane + k * LPE;
+        prw[k] = gptr(P.pairs)[t < E * (E - 1) / 2 ? t : 0];
+      }
+    }
+    rec_copy<LPE>((const GAS f32x4*)gptr(P.s.rec) + (size_t)env * P.s.rec_stride16, (f32x4*)lbase, P.s.rec16);
+    esync<LPE>();
+    if (lane < N) {
+      S.dpre[lane] = S.dpost[lane];
+      S.rpre[lane] = S.rpost[lane];
+      if (DYN == 1) {
+        S.ecs[lane] = cos(S.ps[2 * N + lane]);
+        S.ecs[N + lane] = sin(S.ps[2 * N + lane]);
+      }
+    }
+    cstep = S.step[0] + 1;
+    esync<LPE>();
+    if (K.mode == 1) {
+      reset_env<DYN, LPE, NT>(P, S, env, K.cur_new);
+      esync<LPE>();
+      store_state<DYN, LPE, NT>(P, S, lbase, env, true);
+    }
+  }
+  if (K.mode == 1) return;   // launch-uniform: no workgroup barrier is skipped by some waves only
+  if (live) {
+    if (K.emit_edges) {
+      GAS uint8_t* eo = gptr(P.o.edges) + (size_t)env * E * E;
+      const uint64_t m0 = S.step[1] ? 0ull : ego_mask(S, N, L, N);
+      for (int u = lane; u < E * E; u += LPE) {
+        const int a = qdiv<NT>(u, E, P.m_E), b = u - a * E;
+        double d = 0.0;
+        if (a != b) {
+          const int lo = a < b ? a : b, hi = a < b ? b : a;
+          const double xa = lo < N ? S.ps[lo] : S.lm[lo - N];
+          const double ya = lo < N ? S.ps[N + lo] : S.lm[NL + lo - N];
+          const double xb = hi < N ? S.ps[hi] : S.lm[hi - N];
+          const double yb = hi < N ? S.ps[N + hi] : S.lm[NL + hi - N];
+          const double dx = xa - xb, dy = ya - yb;
+          d = sqrt(dx * dx + dy * dy);
+        }
+        if (((m0 >> a) | (m0 >> b)) & 1ull) d = 0.0;
+        eo[u] = (d <= P.coord_range && d > 0) ? 1 : 0;
+      }
+    }
+    if (lane < N) decode_action(P, S, N, lane, act);
+    filter_on = S.cur[C_FILT] != 0.0;
+    if (filter_on) {
+      const SepChain sc = sep_chain(S.sep);
+      for (int p = lane; p < N * N; p += LPE) {
+        const int i = p / N, j = p - i * N;
+        if (i == j || S.dpre[i] || S.dpre[j]) continue;
+        const double ex = S.ps[i], ey = S.ps[N + i], ox = S.ps[j], oy = S.ps[N + j];
+        S.dpair[p] = sqrt((ox - ex) * (ox - ex) + (oy - ey) * (oy - ey));
+        double rel[5];
+        rel_state<DYN>(S, N, i, j, rel);
+        float v = 0.0f;
+        bool ok;
+        if (DYN == 0) ok = interp_value<4>(P.val, rel, v, sc); else ok = interp_value<5>(P.val, rel, v, sc);
+        S.vpair[p] = ok ? v : INFINITY;
+        S.inr[p] = ok ? 1 : 0;
+      }
+    }
+  }
+  TSTAMP(6);
+  __syncthreads();
+  TSTAMP(1);
+
+  // ---- B. filter + integration, one lane per (env, agent) ------------------------------------
+  if (w == WB) {
+    if (alane) filter_agent<DYN, NT>(P, A, N, ai, A.cur[C_FILT] != 0.0);
+    esync<LPE>();   // every filter of the env has read the pre-step state
+    TSTAMP(9);
+    if (alane && !A.dpre[ai]) integrate_agent<DYN>(P, A, N, ai);
+  }
+  __syncthreads();
+  TSTAMP(2);
+
+  // ---- C. distances; contact forces and magnetic-field sums when asked ------------------------
+  const bool chunked = (E & 3) == 0 && !P.adj_compact;
+  uint64_t m_pre = 0;
+  if (live) {
+    compute_dist<LPE, NT>(P, S, PRE ? prw : nullptr);
+    if (P.o.cforce && lane < N) {
+      double fx, fy;
+      collision_force_agent(S, N, lane, fx, fy);
+      GAS double* cf = gptr(P.o.cforce) + ((size_t)env * N + lane) * 2;
+      cf[0] = fx;
+      cf[1] = fy;
+    }
+    if (DYN == 0 && !P.use_filter_arg) {
+      // partial sums in U2; the per-agent result parks in wnew (info_agent's, written after use)
+      const double mag = magnetic_penalty_wave<LPE, NT>(P, S, S.dpair);
+      if (lane < N) S.wnew[lane] = mag;
+    }
+    m_pre = chunked ? ego_mask(S, N, L, -1) : 0;
+  }
+  TSTAMP(7);
+  __syncthreads();
+  TSTAMP(3);
+
+  // ---- D. per-agent reward / info / stats (agent wave WD) while the other waves store their
+  // env's adjacency speculatively (valid unless an agent changes done / reached status this step:
+  // phase E then rewrites it). WD stores its own in E. (Splitting WD's env's egos over the other
+  // waves in D was measured slower: 36.6 vs 34.5 us at config 3, G = 4.)
+  if (w == WD) {
+    AgentTmp at;
+    if (alane) {
+      min_relative(A, N, ai);
+      const double mag = (DYN == 0 && !P.use_filter_arg) ? A.wnew[ai] : 0.0;
+      reward_agent<DYN, NT>(P, A, aenv, ai, mag, at);
+    }
+    esync<LPE>();   // every agent's goal / done update before the snapshot masks
+    TSTAMP(10);
+    const int acstep = A.step[0] + 1;
+    if (alane) {
+      A.emask[ai] = ego_mask(A, N, L, ai);
+      info_agent<DYN, NT>(P, A, ai, acstep, at, collision_count(A, N, ai));
+    }
+    esync<LPE>();
+    TSTAMP(11);
+    if (alane) {
+      info_row<NT>(P, A, ai, at.rew, A.dpair + ai * LSM_INFO_FIELDS);   // staged in U2
+      episode_stats<DYN>(P, A, N, ai);
+    }
+  } else if (live && chunked) {
+    emit_adj_uniform<LPE, NT>(P, S, env, m_pre, 0, N);
+  }
+  TSTAMP(8);
+  __syncthreads();
+  TSTAMP(4);
+
+  // ---- E. info rows, dones, then the auto-reset or what the speculation did not cover ----------
+  if (!live) return;
+  rec_copy<LPE>((const f32x4*)S.dpair, (GAS f32x4*)(gptr(P.o.info) + (size_t)env * N * LSM_INFO_FIELDS),
+                N * LSM_INFO_FIELDS / 2);
+  bool my_done = true;
+  if (lane < N) {
+    my_done = S.dpost[lane] || cstep >= P.episode_length;
+    gptr(P.o.dones)[(size_t)env * N + lane] = my_done ? 1 : 0;
+  }
+  const bool all_done = __all(my_done);
+  write_masks(P, env, N, lane, my_done, all_done);
+  esync<LPE>();   // info rows read out of U2 before the node rows / a reset overwrite it
+  if (lane == 0) { S.step[0] = cstep; S.step[1] = 0; }
+  if (P.auto_reset && all_done) {
+    if (lane == 0) gptr(P.o.reset_flag)[env] = 1;
+    reset_env<DYN, LPE, NT>(P, S, env, K.cur_new);
+    esync<LPE>();
+    store_state<DYN, LPE, NT>(P, S, lbase, env, true);
+  } else {
+    if (lane == 0) gptr(P.o.reset_flag)[env] = 0;
+    // adjacency already stored in D except WD's (emit_graph rewrites it if a status changed)
+    emit_graph<DYN, LPE, NT>(P, S, env, chunked && w != WD);
+    esync<LPE>();
+    store_state<DYN, LPE, NT>(P, S, lbase, env, false);
+  }
+  TSTAMP(5);
+  TRTSTAMP(14);
+}
+

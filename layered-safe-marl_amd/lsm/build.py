@@ -15,7 +15,7 @@ OUT = os.path.join(CSRC, "liblsm_rollout.so")
 HDR = os.path.join(os.path.dirname(os.path.dirname(HERE)), "include", "lsm_rollout.h")
 # translation units -> their dependencies (each compiled to its own object, then linked)
 UNITS = {
-    "lsm_rollout.hip": ["lsm_numeric.h", "lsm_scenario.h", "lsm_block.h", "lsm_rk45.h", "lsm_pow_tables.h"],
+    "lsm_rollout.hip": ["lsm_numeric.h", "lsm_scenario.h", "lsm_block.h", "lsm_rk45.h", "lsm_pow_tables.h", "lsm_team.h"],
     "lsm_edges.hip": [],
     "lsm_buffer.hip": [],
 }
@@ -66,5 +66,26 @@ def build(force: bool = False, verbose: bool = True) -> str:
     return OUT
 
 
+def build_variant(name: str, defines, verbose: bool = True) -> str:
+    """A/B experiments: the rollout TU rebuilt with extra -D flags and linked with the product's
+    other objects into csrc/liblsm_rollout_<name>.so (select it with LSM_LIB=...). Never the
+    product library."""
+    build(verbose=verbose)
+    out = os.path.join(CSRC, "liblsm_rollout_%s.so" % name)
+    obj = out[:-3] + ".o"
+    cmd = [HIPCC] + FLAGS + ["-D%s" % d for d in defines] + ["-c", "-o", obj, "lsm_rollout.hip"]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.check_call(cmd, cwd=CSRC)
+    objs = [obj] + [_obj(u) for u in UNITS if u != "lsm_rollout.hip"]
+    subprocess.check_call([HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", out] + objs, cwd=CSRC)
+    os.remove(obj)
+    return out
+
+
 if __name__ == "__main__":
-    build(force="--force" in sys.argv)
+    if len(sys.argv) > 2 and sys.argv[1] == "variant":
+        # python -m lsm.build variant NAME DEF1 [DEF2 ...]
+        build_variant(sys.argv[2], sys.argv[3:])
+    else:
+        build(force="--force" in sys.argv)

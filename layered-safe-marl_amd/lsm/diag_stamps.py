@@ -34,6 +34,8 @@ def main():
     ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--build", action="store_true")
     ap.add_argument("--envs", type=int, default=0)
+    ap.add_argument("--team", action="store_true",
+                    help="the team kernel's stamps (lsm_team.h): phases A-E, work vs barrier wait")
     a = ap.parse_args()
     if a.build or not os.path.exists(STAMP_LIB):
         build_stamps()
@@ -59,16 +61,38 @@ def main():
                                        stamps.numel() * 8), env.h)
     env.reset(4)
     N = c["num_agents"]
-    acc, rt = [], []
+    acc, rt, tstamps, tstamps12 = [], [], [], []
     for t in range(a.steps + 10):
         act = torch.randint(0, 25, (n_envs, N), device="cuda:0", dtype=torch.int32)
         env.step(act, 4)
         torch.cuda.synchronize()
         if t >= 10:
             s = stamps.cpu().numpy().astype(np.float64)
+            tstamps.append(s[:, :9].copy())
+            tstamps12.append(s[:, :12].copy())
+            stamps.zero_()
             acc.append(np.diff(s[:, [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10]], axis=1))
             t0 = s[:, 13].min()
             rt.append(np.stack([s[:, 13] - t0, s[:, 14] - t0], axis=1) * 10.0)   # ns (100 MHz)
+    if a.team:
+        # 0 start, 6 A done, 1 after W1, 2 after W2 (B), 7 C done, 3 after W3, 8 D done, 4 after W4, 5 end
+        segs = [("A work", 0, 6), ("A wait", 6, 1), ("B (agent wave)", 1, 2), ("C work", 2, 7),
+                ("C wait", 7, 3), ("D own work", 3, 8), ("D wait", 8, 4), ("E", 4, 5)]
+        allst = np.concatenate(tstamps, axis=0)
+        print("team phase          median cycles   share   p90")
+        tot = np.median(allst[:, 5] - allst[:, 0])
+        for name, i, j in segs:
+            v = allst[:, j] - allst[:, i]
+            print("%-18s %12.0f   %5.1f%%  %8.0f" % (name, np.median(v), 100 * np.median(v) / tot,
+                                                      np.percentile(v, 90)))
+        print("%-18s %12.0f" % ("total", tot))
+        ag = np.concatenate(tstamps12, axis=0)
+        for name, i, j in [("B filter", 1, 9), ("B integrate", 9, 2), ("D reward", 3, 10),
+                           ("D info", 10, 11), ("D rows+stats", 11, 8)]:
+            v = ag[:, j] - ag[:, i]
+            v = v[(ag[:, i] != 0) & (ag[:, j] != 0)]
+            print("%-18s %12.0f   (agent-wave rows: %d)" % (name, np.median(v), len(v)))
+        acc = [np.zeros((1, 10))]
     d = np.concatenate(acc, axis=0)
     med = np.median(d, axis=0)
     tot = med.sum()
