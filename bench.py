@@ -368,8 +368,7 @@ def main():
             "ranks": {"rccl_world_size": (dist.get_world_size() if world > 1 else 1), "ms_per_step": per_rank},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
                          "frac": achieved / PEAK_HBM_GBPS, "traffic": traffic, "traffic_unit": "HBM bytes/launch (rocprofv3 PMC)",
-                         "kernel": "%s<%d>" % ("rollout_block_kernel" if sb["block"] else "rollout_kernel",
-                                               0 if c["dynamics_type"] == "double_integrator" else 1),
+                         "kernel": env.kernel_name,
                          "kernel_ms": kern_ms, "algorithmic_bytes_per_launch": bytes_launch,
                          "gather_bytes_per_launch": sb["gather_bytes"] * n_envs,
                          "bytes_model": "lsm/perf_model.py: record + outputs + HJ gathers (SURVEY 8(d))"},

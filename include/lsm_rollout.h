@@ -70,8 +70,33 @@ enum {
   LSM_OUT_ACTIVE_MASKS = 14, /* float32 [n][N] done ? all(env dones) : 1                 */
   LSM_OUT_COLLISION_FORCE = 15, /* float64 [n][N][2] contact force per agent, written only with
                                    lsm_config.collision_forces (core.py:741-774; never applied) */
-  LSM_NUM_OUT = 16
+  LSM_OUT_DEPARTED = 16,  /* uint8   [n][N]   agent.departed after the call (info 'Departed',
+                             navigation_graph_safe.py:446); written when bound                 */
+  LSM_NUM_OUT = 17
 };
+
+/* Scenario sources (lsm_config.scenario).
+ *  LSM_SCENARIO_TRAIN       the training Scenario.random_scenario drawn on the device at every
+ *                           reset (navigation_graph_safe.py:1199-1367), auto-reset allowed.
+ *  LSM_SCENARIO_LAYOUT      evaluation layouts (navigation_graph_safe_eval.py Scenario): the host
+ *                           computes each reset's agent states / landmarks and passes them to
+ *                           lsm_reset_layout; SafeAamScenario step semantics (departed = True).
+ *  LSM_SCENARIO_DEPARTURES  RealisticScenario layouts (navigation_graph_safe_bayarea_*.py): as
+ *                           LAYOUT plus per-agent departure timers and the RealisticScenario goal /
+ *                           departure update (navigation_graph_safe.py:1153-1186); airtaxi only
+ *                           (its reset_velocity(theta, speed) exists only for KinematicVehicleXY).
+ * Layout scenarios are evaluation paths (scripts/eval_mpe.py forces n_rollout_threads = 1,
+ * GraphDummyVecEnv): they need auto_reset = 0, N <= 32 and N * (1 + L) <= 64, and run the
+ * generic one-wave kernel. */
+enum { LSM_SCENARIO_TRAIN = 0, LSM_SCENARIO_LAYOUT = 1, LSM_SCENARIO_DEPARTURES = 2 };
+
+/* Random streams of the device reset (lsm_config.rng, training scenario).
+ *  LSM_RNG_MT19937  draw-exact replay of numpy's legacy MT19937 stream of env k
+ *                   (np.random.seed(seed + 1000 k)): resets identical to the reference's.
+ *  LSM_RNG_PHILOX   fast mode: Philox4x32-10 keyed by (seed + 1000 k), counter = (reset index,
+ *                   draw index); the same scenario distribution, not the reference's draws. No
+ *                   624-word state is read, twisted or written back at a reset. */
+enum { LSM_RNG_MT19937 = 0, LSM_RNG_PHILOX = 1 };
 
 /* Adjacency output layouts (lsm_config.adj_layout).
  *  0  reference: adj[e][r][c] per ego, what graph_observation returns
@@ -109,7 +134,9 @@ typedef struct lsm_config {
   int32_t collision_forces;  /* 1: report World.get_entity_collision_force per agent each step
                                 (LSM_OUT_COLLISION_FORCE). The reference has no caller for it
                                 (core.py:741-836), so it never changes the dynamics. Default 0. */
-  int32_t reserved0;
+  int32_t scenario;          /* LSM_SCENARIO_TRAIN (default) / _LAYOUT / _DEPARTURES            */
+  int32_t rng;               /* LSM_RNG_MT19937 (default) / LSM_RNG_PHILOX                      */
+  int32_t reserved1;
 } lsm_config;
 
 /* Curriculum block for one reset call (navigation_graph_safe.py:324-366), computed by the
@@ -156,6 +183,19 @@ int lsm_reset(lsm_env* env, const lsm_curriculum* cur, void* hip_stream);
 int lsm_step(lsm_env* env, const void* actions_device, int32_t action_kind,
              const lsm_curriculum* cur_for_auto_reset, void* hip_stream);
 
+/* Reset of a layout scenario (LSM_SCENARIO_LAYOUT / _DEPARTURES): MultiAgentGraphEnv.reset
+ * (environment.py:1046-1074) with random_scenario replaced by the host-computed layout of each
+ * env -- an evaluation Scenario's random_scenario (navigation_graph_safe_eval.py:32-50,
+ * navigation_graph_safe_bayarea_merge.py:63-69, navigation_graph_safe_bayarea_cross.py:59-65),
+ * which draws from the env's numpy stream on the host. `layout` is a DEVICE pointer to float64
+ * [n][lsm_layout_doubles(env)]: agent state [N][4] (x, y, v_x|theta, v_y|speed), landmarks
+ * [N*L][4] (x, y, heading, speed; landmark k = order * N + agent), and with
+ * LSM_SCENARIO_DEPARTURES departed [N] (0/1), departure_timer [N], init_theta [N]. Everything
+ * else of the reset (episode summary, curriculum block, HJ separation shift, goal_min_time, the
+ * observation outputs) is the device's, as in lsm_reset. */
+int lsm_reset_layout(lsm_env* env, const lsm_curriculum* cur, const double* layout_device, void* hip_stream);
+int32_t lsm_layout_doubles(const lsm_env* env);
+
 /* Overwrite the agent states ([N][4], the LSM_OUT_STATE layout) and, if non-null,
  * reached_goal ([N]) of one env between calls -- what scripts do to `world.agents[i].state` /
  * `scenario.reached_goal` between env.step calls (e.g. tests/golden/make_golden.py's injection,
@@ -179,6 +219,11 @@ int lsm_select_ring(lsm_env* env, int32_t index);
  * input), else 0; -1 on error. Synchronises `hip_stream` and clears the flag. */
 int32_t lsm_action_errors(lsm_env* env, void* hip_stream);
 
+/* Name of the kernel instantiation lsm_step / lsm_reset launch for this handle (e.g.
+ * "rollout_team_kernel<0, 8, 4>"), as rocprofv3 reports it without the namespace. Owned by the
+ * library, valid until the next call on the same thread. */
+const char* lsm_kernel_name(const lsm_env* env);
+
 /* Shape helpers. */
 int32_t lsm_num_entities(const lsm_env* env);   /* E = N * (1 + L) */
 int32_t lsm_node_features(const lsm_env* env);  /* F */
@@ -187,11 +232,19 @@ int32_t lsm_obs_dim(const lsm_env* env);        /* OBS */
 /* Host-side entry points of the SAME scenario-generation / RNG code the reset kernel runs
  * (no GPU needed): used by CPU tests against numpy's legacy RandomState. */
 int lsm_host_mt_uniforms(uint32_t seed, int32_t count, double lo, double hi, double* out);
+/* The fast-mode (LSM_RNG_PHILOX) stream of reset `reset_index` of an env keyed `key`
+ * (= seed + 1000 k): uniform(lo, hi) draws in order. */
+int lsm_host_philox_uniforms(uint32_t key, uint32_t reset_index, int32_t count, double lo, double hi,
+                             double* out);
+/* The raw Philox4x32-10 block function (ctr [4], key [2] -> out [4]): Random123 known answers. */
+int lsm_host_philox4x32(const uint32_t* ctr, const uint32_t* key, uint32_t* out);
 /* The double integrator's step as the kernel computes it: scipy's solve_ivp(x' = v, v' = a,
  * [0, dt], y0, 'RK45').y[:, -1] restated operation for operation (core.py:199-210); returns the
  * number of RK45 steps. lsm_host_glibc_pow: the kernel's restatement of glibc's pow. */
 int lsm_host_rk45_di(const double* y0 /* [4] */, double a0, double a1, double dt, double* y_out /* [4] */);
 double lsm_host_glibc_pow(double x, double y);
+/* random_scenario as the device draws it for the first reset of an env seeded `seed`
+ * (cfg->rng: MT19937 replay, or the Philox stream of reset index 0). */
 int lsm_host_scenario(const lsm_config* cfg, const lsm_curriculum* cur, uint32_t seed,
                       double* agent_state /* [N][4] */, double* landmarks /* [NL][4] */);
 

@@ -160,4 +160,49 @@ struct HostMT {
   }
 };
 
+// ---- Philox4x32-10 (Salmon et al., SC'11): the fast reset stream (LSM_RNG_PHILOX) ----------
+// Counter-based: draw block b of reset r of env key k is philox(ctr = (b, r, 0, 0), key = (k, tag)),
+// so a reset needs no stored generator state (the device keeps only r). Every lane of an env
+// runs the identical scalar sequence, like the MT19937 replay. Doubles take two words the
+// numpy way ((a >> 5) 2^26 + (b >> 6)) / 2^53, so uniform(lo, hi) has the same form.
+// The Philox4x32 block function, 10 rounds (Random123's philox4x32_R(10, ctr, key)).
+LSM_HD void philox4x32_10(const uint32_t* ctr, const uint32_t* key, uint32_t* out) {
+  uint32_t c0 = ctr[0], c1 = ctr[1], c2 = ctr[2], c3 = ctr[3], a = key[0], b = key[1];
+  for (int i = 0; i < 10; ++i) {
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
+    const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ a, n2 = (uint32_t)(p0 >> 32) ^ c3 ^ b;
+    c1 = (uint32_t)p1; c3 = (uint32_t)p0; c0 = n0; c2 = n2;
+    a += 0x9E3779B9u; b += 0xBB67AE85u;
+  }
+  out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+struct Philox {
+  uint32_t k0, k1, r;   // key, reset index
+  uint32_t blk;         // next counter block
+  uint32_t buf[4];
+  int pos;
+  LSM_HD void init(uint32_t key, uint32_t reset_index) {
+    k0 = key; k1 = 0x4c534d31u; r = reset_index; blk = 0; pos = 4;
+  }
+  LSM_HD void round_all() {
+    const uint32_t ctr[4] = {blk, r, 0u, 0u}, key[2] = {k0, k1};
+    philox4x32_10(ctr, key, buf);
+    ++blk;
+    pos = 0;
+  }
+  LSM_HD uint32_t next32() {
+    if (pos >= 4) round_all();
+    return buf[pos++];
+  }
+  LSM_HD double next_double() {
+    uint32_t a = next32() >> 5, b = next32() >> 6;
+    return (a * 67108864.0 + b) / 9007199254740992.0;
+  }
+  LSM_HD double uniform(double lo, double hi) {
+    double range = hi - lo;
+    return lo + range * next_double();
+  }
+};
+
 }  // namespace lsm

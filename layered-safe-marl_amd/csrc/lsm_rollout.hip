@@ -114,7 +114,9 @@ struct StateDev {
   uint32_t rec16;       // float4 per record
   uint32_t hot16;       // float4 rewritten every step (up to cur)
   double* prev;         // [n][8] previous episode summary
-  uint32_t* mt;         // [n][MT_WORDS]
+  uint32_t* mt;         // [n][MT_WORDS] (LSM_RNG_PHILOX: only word MT_N, the reset index + MT_N)
+  double* dep;          // [n][DEPW(N)] departed [N], departure_timer [N], init_theta [N], and the
+                        // final disconnect mask of the last call (u64 bits) (LSM_SCENARIO_DEPARTURES)
 };
 
 struct OutDev {
@@ -133,12 +135,17 @@ struct OutDev {
   float* masks;        // LSM_OUT_MASKS (optional)
   float* active_masks; // LSM_OUT_ACTIVE_MASKS (optional)
   double* cforce;      // LSM_OUT_COLLISION_FORCE (lsm_config.collision_forces only)
+  uint8_t* departed;   // LSM_OUT_DEPARTED (optional)
 };
 
 struct KParams {
   int n_envs, N, L, NL, E, F, OBS, dyn, episode_length, use_masking, use_filter_arg, auto_reset;
   int adj_compact;   // LSM_ADJ_COMPACT: unmasked E x E table once per env + per-ego masks
   int filter_search; // workgroup kernel's HJ argmin: 1 bound-pruned (default), 0 every pair exact
+  int scenario;      // LSM_SCENARIO_*
+  int rng;           // LSM_RNG_*
+  int64_t seed, env_offset;   // Philox keys: seed + 1000 * (env_offset + env)
+  uint32_t lds_dep_off;       // LSM_SCENARIO_DEPARTURES: LDS offset of the departure arrays
   double dt, world_size, coord_range, world_eng, sep_target, max_speed, min_speed, gs_min, gs_max;
   double coord_range2;   // coord_range^2 (float64-rounded)
   double act0[5], act1[5];
@@ -163,7 +170,8 @@ struct KParams {
 // Per-launch kernel arguments (the rest lives in a device-resident KParams per handle).
 struct KStep {
   const void* actions;
-  int action_kind, mode, emit_edges, stop_after;   // mode 0 = step, 1 = reset all
+  const double* layout;   // mode 2: [n][layout doubles] (lsm_reset_layout)
+  int action_kind, mode, emit_edges, stop_after;   // mode 0 = step, 1 = reset all, 2 = reset from layout
   double cur_new[NCUR];
 };
 
@@ -173,6 +181,8 @@ struct KStep {
 //   U1 = {fval, aa, aa2} (step)         | {mt, scen, scratch} (reset) | {stage} (node output, last)
 //   U2 = {dpair, vpair, inr} (filter)   | {feat, egooff} (DI node rows) | magnetic partial sums
 // ----------------------------------------------------------------------------------
+__host__ __device__ inline size_t align16_(size_t x) { return (x + 15) & ~(size_t)15; }
+
 struct Lds {
   // ---- persistent record (StateDev) ----
   double* ps;        // [4][N] agent state (after integration; velocities pre-freeze)
@@ -221,7 +231,24 @@ struct Lds {
   int32_t* ccnt;     // [N] is_collision counts of this step
   uint64_t* mpre;    // [4] disconnect bits before the reward update (entity r = bit r)
   uint64_t* mpost;   // [4] after
+  // LSM_SCENARIO_DEPARTURES only (generic airtaxi one-wave kernel; nullptr elsewhere, so every
+  // departure test below folds away in the other kernels)
+  int32_t* dep0;     // [N] departed before the reward update
+  int32_t* dep1;     // [N] after
+  int32_t* tmr;      // [N] departure_timer
+  double* ith;       // [N] init_theta
+  double* pth;       // [N] heading after the reward update (departure resets it)
+  double* psp;       // [N] speed after the reward update (departure / freeze / done)
+  double* trig1;     // [4][N] cos, sin, vx, vy of the post state (node features)
 };
+
+// doubles per env of StateDev::dep
+__host__ __device__ inline int depw(int N) { return 3 * N + 1; }
+
+// LDS bytes of the departure arrays (appended after lds_plan's block)
+__host__ __device__ inline size_t dep_lds_bytes(int N) {
+  return 3 * align16_(4 * (size_t)N) + 3 * align16_(8 * (size_t)N) + align16_(32 * (size_t)N);
+}
 
 struct LdsPlan {
   size_t bytes;     // LDS per env
@@ -421,7 +448,20 @@ __device__ __forceinline__ Lds carve(unsigned char* base, int N, int NL, int E, 
   L.ex = L.ey = nullptr;
   L.ccnt = nullptr;
   L.mpre = L.mpost = nullptr;
+  L.dep0 = L.dep1 = L.tmr = nullptr;
+  L.ith = L.pth = L.psp = L.trig1 = nullptr;
   return L;
+}
+
+// The departure arrays of an env block (LSM_SCENARIO_DEPARTURES) at byte offset `off`.
+__device__ __forceinline__ void carve_dep(Lds& L, unsigned char* base, size_t off, int N) {
+  L.dep0 = (int32_t*)(base + off); off += align16_(4 * (size_t)N);
+  L.dep1 = (int32_t*)(base + off); off += align16_(4 * (size_t)N);
+  L.tmr = (int32_t*)(base + off); off += align16_(4 * (size_t)N);
+  L.ith = (double*)(base + off); off += align16_(8 * (size_t)N);
+  L.pth = (double*)(base + off); off += align16_(8 * (size_t)N);
+  L.psp = (double*)(base + off); off += align16_(8 * (size_t)N);
+  L.trig1 = (double*)(base + off);
 }
 
 // LDS carve of the workgroup-per-env kernel (lds_plan(..., block = true)).
@@ -467,6 +507,8 @@ __device__ __forceinline__ Lds carve_block(unsigned char* base, int N, int NL, i
   L.dpair = (double*)(base + p.off[k++]);
   L.stage = (float*)(base + p.off[k++]);
   L.fval = nullptr; L.aa = nullptr; L.aa2 = nullptr; L.vpair = nullptr; L.inr = nullptr;
+  L.dep0 = L.dep1 = L.tmr = nullptr;
+  L.ith = L.pth = L.psp = L.trig1 = nullptr;
   return L;
 }
 
@@ -754,9 +796,21 @@ __device__ __forceinline__ int goal_index(int reached, int j, int N, int NL) {
 }
 
 // agent j velocity components for a given "post" choice.
+// Agent j "inactive" in World.step before the reward update: done, or not departed yet
+// (core.py:655, 669, 685, 700-705: `agent.done or not agent.departed`).
+__device__ __forceinline__ bool inactive_pre(const Lds& S, int j) {
+  return S.dpre[j] || (S.dep0 && !S.dep0[j]);
+}
+
 template <int DYN>
 __device__ __forceinline__ void agent_vel(const Lds& S, int N, int j, bool post, double& vx, double& vy) {
   const bool frozen = post && S.dpost[j];
+  if (DYN == 1 && post && S.psp) {   // departures: the post state carries departure / freezes
+    const double th = S.pth[j], sp = S.psp[j];
+    vx = sp * cos(th);
+    vy = sp * sin(th);
+    return;
+  }
   if (DYN == 0) {
     vx = frozen ? 0.0 : S.ps[2 * N + j];
     vy = frozen ? 0.0 : S.ps[3 * N + j];
@@ -771,6 +825,7 @@ __device__ __forceinline__ void agent_vel(const Lds& S, int N, int j, bool post,
 template <int DYN>
 __device__ __forceinline__ double agent_speed(const Lds& S, int N, int j, bool post) {
   const bool frozen = post && S.dpost[j];
+  if (DYN == 1 && post && S.psp) return S.psp[j];
   if (DYN == 0) {
     const double vx = frozen ? 0.0 : S.ps[2 * N + j];
     const double vy = frozen ? 0.0 : S.ps[3 * N + j];
@@ -933,7 +988,7 @@ __device__ __forceinline__ void filter_ego(const KParams& P, Lds& S, int i, uint
   double dmin = 0.0;
   float vmin = 0.0f;
   for (int j = 0; j < N; ++j) {
-    if (j == i || S.dpre[j]) continue;
+    if (j == i || inactive_pre(S, j)) continue;
     const double d = S.dpair[i * N + j];
     const float v = S.vpair[i * N + j];
     if (jd < 0 || d < dmin) { jd = j; dmin = d; }
@@ -1106,14 +1161,22 @@ __device__ __forceinline__ void node_features(const KParams& P, const Lds& S, in
   const double* ts = S.feat + N;        // sin th [N]
   const double* tvx = S.feat + 2 * N;   // unfrozen velocity [N]
   const double* tvy = S.feat + 3 * N;
+  // departures: post-update rows (heading / speed after a departure, waiting freeze or done
+  // freeze) in trig1; otherwise the post state differs from the pre state only by the done freeze
+  const bool dm = DYN == 1 && S.trig1 != nullptr;
+  const double* tc1 = dm ? S.trig1 : tc;
+  const double* ts1 = dm ? S.trig1 + N : ts;
+  const double* tvx1 = dm ? S.trig1 + 2 * N : tvx;
+  const double* tvy1 = dm ? S.trig1 + 3 * N : tvy;
   const double pex = S.ps[e], pey = S.ps[N + e];
-  const double c = tc[e], s = ts[e];
-  const bool efz = S.dpost[e] != 0;     // the ego is seen after its own update
-  const double vex = efz ? 0.0 : tvx[e], vey = efz ? 0.0 : tvy[e];
+  const double c = tc1[e], s = ts1[e];
+  const bool efz = !dm && S.dpost[e] != 0;     // the ego is seen after its own update
+  const double vex = efz ? 0.0 : tvx1[e], vey = efz ? 0.0 : tvy1[e];
   if (k < N) {
     const bool post = k <= e;
-    const bool kfz = post && S.dpost[k];
-    const double vkx = kfz ? 0.0 : tvx[k], vky = kfz ? 0.0 : tvy[k];
+    const bool kfz = !dm && post && S.dpost[k];
+    const double vkx = kfz ? 0.0 : (post ? tvx1 : tvx)[k], vky = kfz ? 0.0 : (post ? tvy1 : tvy)[k];
+    const double ck = (post ? tc1 : tc)[k], sk = (post ? ts1 : ts)[k];
     const int gi = goal_index(post ? S.rpost[k] : S.rpre[k], k, N, NL);
     double rx, ry, gx, gy;
     blas_rot(c, s, S.ps[k] - pex, S.ps[N + k] - pey, rx, ry);
@@ -1123,8 +1186,8 @@ __device__ __forceinline__ void node_features(const KParams& P, const Lds& S, in
     f[0] = (float)rx;
     f[1] = (float)ry;
     f[2] = (float)rs;
-    f[3] = (float)(ts[k] * c - tc[k] * s);   // sin(th_k - th_e)
-    f[4] = (float)(tc[k] * c + ts[k] * s);   // cos(th_k - th_e)
+    f[3] = (float)(sk * c - ck * s);   // sin(th_k - th_e)
+    f[4] = (float)(ck * c + sk * s);   // cos(th_k - th_e)
     f[5] = (float)gx;
     f[6] = (float)gy;
     f[7] = (float)(sg * c - cg * s);
@@ -1139,7 +1202,7 @@ __device__ __forceinline__ void node_features(const KParams& P, const Lds& S, in
     const float sn = (float)(sl * c - cl * s), cs = (float)(cl * c + sl * s);
     f[0] = (float)rx;
     f[1] = (float)ry;
-    f[2] = (float)(efz ? 0.0 : S.ps[3 * N + e]);
+    f[2] = (float)(dm ? S.psp[e] : (efz ? 0.0 : S.ps[3 * N + e]));
     f[3] = sn;
     f[4] = cs;
     f[5] = (float)rx;
@@ -1164,6 +1227,14 @@ __device__ __forceinline__ void trig_table_at(const KParams& P, Lds& S) {
     S.feat[N + j] = sn;
     S.feat[2 * N + j] = sp * c;
     S.feat[3 * N + j] = sp * sn;
+    if (S.trig1) {
+      const double th1 = S.pth[j], sp1 = S.psp[j];
+      const double c1 = cos(th1), s1 = sin(th1);
+      S.trig1[j] = c1;
+      S.trig1[N + j] = s1;
+      S.trig1[2 * N + j] = sp1 * c1;
+      S.trig1[3 * N + j] = sp1 * s1;
+    }
   }
 }
 
@@ -1175,6 +1246,7 @@ __device__ __forceinline__ uint64_t ego_mask(const Lds& S, int N, int L, int e) 
   for (int j = 0; j < N; ++j) {
     const bool post = j <= e;
     if (post ? S.dpost[j] : S.dpre[j]) m |= 1ull << j;
+    if (S.dep0 && !(post ? S.dep1[j] : S.dep0[j])) m |= 1ull << j;   // not departed (:979)
     const int rg = post ? S.rpost[j] : S.rpre[j];
     for (int o = 0; o < L; ++o)
       if (rg > o) m |= 1ull << (N + o * N + j);
@@ -1277,7 +1349,8 @@ __device__ __forceinline__ void emit_graph(const KParams& P, Lds& S, int env, bo
   // No agent changed done / reached status this step (the common case): every ego then has
   // the same disconnect mask and the same (pre == post) entity rows, so each lane computes
   // its output words once and stores them for all N egos.
-  const bool uni = group_all<LPE>(lane >= N || (S.dpre[lane] == S.dpost[lane] && S.rpre[lane] == S.rpost[lane]));
+  const bool uni = !S.dep0 &&
+                   group_all<LPE>(lane >= N || (S.dpre[lane] == S.dpost[lane] && S.rpre[lane] == S.rpost[lane]));
   // ---- adjacency: ego e, row r, col c ------------------------------------------------------
   const int EE = E * E, atot = N * EE;
   GAS float* adj_out = gptr(P.o.adj) + (size_t)env * atot;
@@ -1622,7 +1695,8 @@ __device__ __forceinline__ void summary_rolled(const KParams& P, const Lds& S, d
 // Everything of the reset up to the outputs: summary, curriculum block, scenario draw,
 // per-agent episode arrays.
 template <int DYN, int LPE, int NT>
-__device__ __forceinline__ void reset_core(const KParams& P, Lds& S, int env, const double* cur_new) {
+__device__ __forceinline__ void reset_core(const KParams& P, Lds& S, int env, const double* cur_new,
+                                           const double* layout = nullptr) {
   const int lane = threadIdx.x & (LPE - 1);
   LSM_DIMS;
   GAS double* prev = gptr(P.s.prev) + (size_t)env * 8;
@@ -1650,13 +1724,48 @@ __device__ __forceinline__ void reset_core(const KParams& P, Lds& S, int env, co
       S.sep[1] = cur_new[C_SEP];
     }
   }
-  const GAS uint32_t* mtg = gptr(P.s.mt) + (size_t)env * MT_WORDS;
-  for (int k = lane; k < MT_WORDS; k += LPE) S.mt[k] = mtg[k];
-  esync<LPE>();
   ScenarioParams sp;
   sp.dyn = DYN; sp.N = N; sp.L = L; sp.world_size = P.world_size; sp.coordination_range = P.coord_range;
   sp.goal_speed_min = P.gs_min; sp.goal_speed_max = P.gs_max;
   sp.ratio_airtaxi = S.cur[C_RAT]; sp.ratio_scenario = S.cur[C_RSC]; sp.two_pi = P.two_pi; sp.pi = P.pi;
+  if (layout) {
+    // lsm_reset_layout: the host's evaluation layout replaces random_scenario (no device draws)
+    const int LD = 4 * N + 4 * NL + (S.dep0 ? 3 * N : 0);
+    const GAS double* g = gptr(layout) + (size_t)env * LD;
+    for (int k = lane; k < 4 * N; k += LPE) {
+      const int i = k >> 2, c = k & 3;
+      S.ps[c * N + i] = g[k];
+    }
+    for (int k = lane; k < 4 * NL; k += LPE) {
+      const int l = k >> 2, c = k & 3;
+      S.lm[c * NL + l] = g[4 * N + k];
+    }
+    if (S.dep0) {
+      for (int k = lane; k < N; k += LPE) {
+        S.dep0[k] = S.dep1[k] = g[4 * N + 4 * NL + k] != 0.0;
+        S.tmr[k] = (int32_t)g[5 * N + 4 * NL + k];
+        S.ith[k] = g[6 * N + 4 * NL + k];
+      }
+    }
+    esync<LPE>();
+  } else if (P.rng == LSM_RNG_PHILOX) {
+    // fast mode: Philox keyed by the env's seed, counter = this env's reset index (kept in the
+    // MT position word); no 624-word state is read, twisted or written back
+    GAS uint32_t* rw = gptr(P.s.mt) + (size_t)env * MT_WORDS + MT_N;
+    const uint32_t ridx = *rw - (uint32_t)MT_N;
+    const uint32_t key = (uint32_t)(P.seed + 1000 * (P.env_offset + env));
+    esync<LPE>();
+    if (LPE <= WAVE || (int)threadIdx.x < WAVE) {   // workgroup kernel: one wave draws (see below)
+      Philox rng;
+      rng.init(key, ridx);
+      random_scenario(rng, sp, S.ps, S.lm, S.scen);
+    }
+    esync<LPE>();
+    if (lane == 0) *rw = ridx + 1 + (uint32_t)MT_N;
+  } else {
+  const GAS uint32_t* mtg = gptr(P.s.mt) + (size_t)env * MT_WORDS;
+  for (int k = lane; k < MT_WORDS; k += LPE) S.mt[k] = mtg[k];
+  esync<LPE>();
   if (LPE > WAVE) {
     // workgroup kernel: the scenario's read-modify-writes of its LDS workspace are only safe
     // when every writer runs in lockstep, so one wave draws it (the others wait below)
@@ -1680,6 +1789,7 @@ __device__ __forceinline__ void reset_core(const KParams& P, Lds& S, int env, co
   }
   GAS uint32_t* mtw = gptr(P.s.mt) + (size_t)env * MT_WORDS;
   for (int k = lane; k < MT_WORDS; k += LPE) mtw[k] = S.mt[k];
+  }
   for (int k = lane; k < NL; k += LPE) {
     S.lmsc[k] = sin(S.lm[2 * NL + k]);
     S.lmsc[NL + k] = cos(S.lm[2 * NL + k]);
@@ -1694,13 +1804,23 @@ __device__ __forceinline__ void reset_core(const KParams& P, Lds& S, int env, co
   }
   if (lane == 0) { S.step[0] = 0; S.step[1] = 0; }
   esync<LPE>();   // MT words read out of U1 before compute_dist overwrites it
+  if (S.dep0) {
+    // departures: undeparted agents are disconnected from the reset's graph observation too
+    for (int k = lane; k < N; k += LPE) {
+      S.pth[k] = S.ps[2 * N + k];
+      S.psp[k] = S.ps[3 * N + k];
+      S.emask[k] = ego_mask(S, N, L, k);
+    }
+    esync<LPE>();
+  }
 }
 
 template <int DYN, int LPE, int NT>
-__device__ __forceinline__ void reset_env(const KParams& P, Lds& S, int env, const double* cur_new) {
+__device__ __forceinline__ void reset_env(const KParams& P, Lds& S, int env, const double* cur_new,
+                                          const double* layout = nullptr) {
   const int lane = threadIdx.x & (LPE - 1);
   LSM_DIMS;
-  reset_core<DYN, LPE, NT>(P, S, env, cur_new);
+  reset_core<DYN, LPE, NT>(P, S, env, cur_new, layout);
   compute_dist<LPE, NT>(P, S, nullptr, true);
   if (lane < N) write_obs<DYN, NT>(P, S, env, lane);
   emit_graph<DYN, LPE, NT>(P, S, env);
@@ -1732,6 +1852,20 @@ __device__ __forceinline__ void store_state(const KParams& P, Lds& S, const unsi
                                             bool full) {
   const int lane = threadIdx.x & (LPE - 1);
   LSM_DIMS;
+  if (DYN == 1 && S.dep0) {
+    // departures: the post-update heading / speed become the state; departure arrays persist
+    GAS double* dg = gptr(P.s.dep) + (size_t)env * depw(N);
+    if (lane == 0) *(GAS uint64_t*)(dg + 3 * N) = S.emask[N - 1];   // next step's update_graph mask
+    for (int j = lane; j < N; j += LPE) {
+      S.ps[2 * N + j] = S.pth[j];
+      S.ps[3 * N + j] = S.psp[j];
+      dg[j] = (double)S.dep1[j];
+      dg[N + j] = (double)S.tmr[j];
+      dg[2 * N + j] = S.ith[j];
+      if (P.o.departed) gptr(P.o.departed)[(size_t)env * N + j] = S.dep1[j] ? 1 : 0;
+    }
+    esync<LPE>();
+  }
   for (int k = lane; k < 4 * N; k += LPE) {
     const int c = k / N, j = k - c * N;
     double v = S.ps[k];
@@ -1903,10 +2037,42 @@ __device__ __forceinline__ void reward_agent(const KParams& P, Lds& S, int env, 
     }
   }
   t.rew = np_clip(r, -40.0, 50.0);
-  int rp = S.rpre[i];
-  if (reached && (!P.use_masking || !done0)) rp += 1;
-  S.rpost[i] = rp;
-  S.dpost[i] = (rp >= L) ? 1 : S.dpre[i];
+  if (DYN == 1 && S.dep0) {
+    // RealisticScenario.update_reached_goal_and_done (navigation_graph_safe.py:1153-1186): the
+    // departure (heading / speed reset once the timer has run out) or the waiting freeze, then
+    // the goal test on the updated state, recursing while goals keep being reached (a layout may
+    // repeat a goal position); at most L + 1 rounds.
+    int dep = S.dep0[i], tm = S.tmr[i], rp = S.rpre[i], dn = S.dpre[i];
+    double th1 = S.ps[2 * N + i], v1 = S.ps[3 * N + i];
+    for (int it = 0; it <= L + 1; ++it) {
+      if (tm <= 0 && !dep) {
+        if (S.minrel[i] > P.sep_target) {   // reset_velocity(theta=init_theta, speed=goal_speed_max)
+          th1 = S.ith[i];
+          v1 = P.gs_max;
+          dep = 1;
+        }
+      } else if (!dep) {
+        tm -= 1;
+        v1 = 0.0;   // freeze_agent (:1091-1099)
+      }
+      const int g2 = goal_index(rp, i, N, NL);
+      if (!goal_reached_at<DYN>(S, N, NL, i, g2, v1, dae(th1, S.lm[2 * NL + g2]))) break;
+      if (!P.use_masking || !dn) rp += 1;
+      if (rp >= L) {   // agent_reached_all_goals: done, frozen
+        dn = 1;
+        v1 = 0.0;
+        break;
+      }
+    }
+    S.dep1[i] = dep; S.tmr[i] = tm; S.pth[i] = th1; S.psp[i] = v1;
+    S.rpost[i] = rp;
+    S.dpost[i] = dn;
+  } else {
+    int rp = S.rpre[i];
+    if (reached && (!P.use_masking || !done0)) rp += 1;
+    S.rpost[i] = rp;
+    S.dpost[i] = (rp >= L) ? 1 : S.dpre[i];
+  }
   gptr(P.o.rew)[(size_t)env * N + i] = (float)t.rew;
 }
 
@@ -1923,7 +2089,10 @@ __device__ __forceinline__ void info_agent(const KParams& P, Lds& S, int i, int 
   const double dist = plain_norm2(S.ps[i] - S.lm[gi], S.ps[N + i] - S.lm[NL + gi]);
   const double pd = S.pdist[i];
   bool reached_post = t.reached_pre;   // same state and goal unless the goal advanced
-  if (S.rpost[i] != S.rpre[i]) {
+  if (DYN == 1 && S.psp) {
+    // departures: the update may have changed heading / speed (departure, freeze)
+    reached_post = goal_reached_at<DYN>(S, N, NL, i, gi, S.psp[i], dae(S.pth[i], S.lm[2 * NL + gi]));
+  } else if (S.rpost[i] != S.rpre[i]) {
     const bool frz = S.dpost[i] != 0;
     const double spp = frz ? 0.0 : t.spd_pre;
     double hep;
@@ -2005,7 +2174,7 @@ __device__ __forceinline__ void stats_agent(const KParams& P, Lds& S, int N, int
 // final disconnect mask S.emask[i] keeps; `departed` is always True in the training scenario.
 template <int DYN>
 __device__ __forceinline__ void episode_stats(const KParams& P, Lds& S, int N, int i) {
-  if (!S.dpost[i]) {
+  if (!S.dpost[i] && (!S.dep1 || S.dep1[i])) {   // `agent.departed and not agent.done` (:1008)
     const uint64_t m = S.emask[i];
     int cnt = 0, neng = 0;
     double mn = INFINITY;
@@ -2025,9 +2194,9 @@ __device__ __forceinline__ void episode_stats(const KParams& P, Lds& S, int N, i
 // min relative distance of agent i over the other active agents (core.py:696-709)
 __device__ __forceinline__ void min_relative(Lds& S, int N, int i) {
   double m = INFINITY;
-  if (!S.dpre[i]) {
+  if (!inactive_pre(S, i)) {
     for (int j = 0; j < N; ++j) {
-      if (j == i || S.dpre[j]) continue;
+      if (j == i || inactive_pre(S, j)) continue;
       const double d = S.aa2[i * N + j];
       m = (d < m) ? d : m;
     }
@@ -2081,7 +2250,7 @@ __device__ __forceinline__ void filter_agent(const KParams& P, Lds& S, int N, in
   if (filter_on) {
     uint8_t fl = 0;
     int dec = -1;
-    if (!S.dpre[i]) filter_ego<DYN, NT>(P, S, i, fl, dec, u0, u1);
+    if (!inactive_pre(S, i)) filter_ego<DYN, NT>(P, S, i, fl, dec, u0, u1);
     S.sfilt[i] = fl;
     S.decon[i] = dec;
   }
@@ -2108,6 +2277,8 @@ __global__ __launch_bounds__(64, DYN == 0 ? (LPE == 64 ? 4 : 2) : LSM_WAVES_PER_
   LSM_DIMS;
   unsigned char* lbase = smem + (size_t)grp * P.lds_env_bytes;
   Lds S = carve(lbase, N, NL, E, F);
+  // RealisticScenario departures run only here: the generic airtaxi kernel, one env per wave
+  if (DYN == 1 && NT == 0 && LPE == 64 && P.scenario == LSM_SCENARIO_DEPARTURES) carve_dep(S, lbase, P.lds_dep_off, N);
   RTSTAMP(13);
 #ifdef LSM_STAMPS
   if (lane == 0 && gptr(P.stamps))
@@ -2139,13 +2310,21 @@ __global__ __launch_bounds__(64, DYN == 0 ? (LPE == 64 ? 4 : 2) : LSM_WAVES_PER_
       S.ecs[lane] = cos(S.ps[2 * N + lane]);
       S.ecs[N + lane] = sin(S.ps[2 * N + lane]);
     }
+    if (S.dep0 && K.mode == 0) {
+      const GAS double* dg = gptr(P.s.dep) + (size_t)env * depw(N);
+      S.dep0[lane] = S.dep1[lane] = dg[lane] != 0.0;
+      S.tmr[lane] = (int32_t)dg[N + lane];
+      S.ith[lane] = dg[2 * N + lane];
+      S.pth[lane] = S.ps[2 * N + lane];
+      S.psp[lane] = S.ps[3 * N + lane];
+    }
   }
   const int cstep = S.step[0] + 1;
   __syncthreads();
   STAMP(1);
 
-  if (K.mode == 1) {
-    reset_env<DYN, LPE, NT>(P, S, env, K.cur_new);
+  if (K.mode != 0) {   // 1: device scenario, 2: host layout (lsm_reset_layout)
+    reset_env<DYN, LPE, NT>(P, S, env, K.cur_new, K.mode == 2 ? K.layout : nullptr);
     __syncthreads();
     store_state<DYN, LPE, NT>(P, S, lbase, env, true);
     return;
@@ -2156,7 +2335,8 @@ __global__ __launch_bounds__(64, DYN == 0 ? (LPE == 64 ? 4 : 2) : LSM_WAVES_PER_
     GAS uint8_t* eo = gptr(P.o.edges) + (size_t)env * E * E;
     // the previous step's observation masked cached_dist_mag in place; after an edit of the
     // state (lsm_set_agent_state = world.calculate_distances()) it is fresh
-    const uint64_t m0 = S.step[1] ? 0ull : ego_mask(S, N, L, N);
+    uint64_t m0 = S.step[1] ? 0ull : ego_mask(S, N, L, N);
+    if (S.dep0 && !S.step[1]) m0 = *(const GAS uint64_t*)(gptr(P.s.dep) + (size_t)env * depw(N) + 3 * N);
     for (int u = lane; u < E * E; u += LPE) {
       const int a = qdiv<NT>(u, E, P.m_E), b = u - a * E;
       double d = 0.0;
@@ -2190,7 +2370,7 @@ __global__ __launch_bounds__(64, DYN == 0 ? (LPE == 64 ? 4 : 2) : LSM_WAVES_PER_
     const int npairs = N * N;
     for (int p = lane; p < npairs; p += LPE) {
       const int i = p / N, j = p - i * N;
-      if (i == j || S.dpre[i] || S.dpre[j]) continue;
+      if (i == j || inactive_pre(S, i) || inactive_pre(S, j)) continue;
       const double ex = S.ps[i], ey = S.ps[N + i], ox = S.ps[j], oy = S.ps[N + j];
       S.dpair[p] = sqrt((ox - ex) * (ox - ex) + (oy - ey) * (oy - ey));
       double rel[5];
@@ -2209,7 +2389,7 @@ __global__ __launch_bounds__(64, DYN == 0 ? (LPE == 64 ? 4 : 2) : LSM_WAVES_PER_
   STAMP(4);
 
   // ---- 4. integrate ----------------------------------------------------------------------
-  if (lane < N && !S.dpre[lane]) integrate_agent<DYN>(P, S, N, lane);
+  if (lane < N && !inactive_pre(S, lane)) integrate_agent<DYN>(P, S, N, lane);
   __syncthreads();
   STAMP(5);
 
@@ -2227,7 +2407,7 @@ __global__ __launch_bounds__(64, DYN == 0 ? (LPE == 64 ? 4 : 2) : LSM_WAVES_PER_
   // ego's mask is the pre-update mask, so the adjacency can be stored now, in four chunks of
   // egos placed between the remaining phases: the stores drain while the wave computes
   // instead of queueing behind each other at the end. A status change rewrites it at the end.
-  const bool chunked = (E & 3) == 0 && !P.adj_compact;
+  const bool chunked = (E & 3) == 0 && !P.adj_compact && !S.dep0;
   const uint64_t m_pre = chunked ? ego_mask(S, N, L, -1) : 0;
   if (chunked) emit_adj_uniform<LPE, NT>(P, S, env, m_pre, 0, N / 4);
   STAMP(6);
@@ -2240,6 +2420,16 @@ __global__ __launch_bounds__(64, DYN == 0 ? (LPE == 64 ? 4 : 2) : LSM_WAVES_PER_
   const double rew = at.rew;
   __syncthreads();
   if (lane < N) S.emask[lane] = ego_mask(S, N, L, lane);
+  if (S.dep0) {
+    // graph_observation masks cached_dist_mag IN PLACE (navigation_graph_safe.py:986-987), so
+    // masks accumulate over the egos of a step. Done / reached only ever disconnect, so for them
+    // ego e's own mask is that union; a departure connects: agent j >= 1 undeparted before the
+    // update was masked by ego 0 and stays masked for every later ego of this step.
+    uint64_t acc = 0;
+    for (int j = 1; j < N; ++j)
+      if (!S.dep0[j]) acc |= 1ull << j;
+    if (lane < N) S.emask[lane] |= acc;
+  }
   if (chunked) emit_adj_uniform<LPE, NT>(P, S, env, m_pre, N / 4, N / 2);
   STAMP(7);
 
@@ -2385,6 +2575,11 @@ static void fill_params(const lsm_env* e, KParams& P) {
   P.adj_compact = e->cfg.adj_layout == LSM_ADJ_COMPACT;
   P.filter_search = 1;
   if (const char* v = getenv("LSM_FILTER_SEARCH")) P.filter_search = atoi(v);
+  P.scenario = e->cfg.scenario;
+  P.rng = e->cfg.rng;
+  P.seed = e->cfg.seed;
+  P.env_offset = e->cfg.env_offset;
+  P.lds_dep_off = (uint32_t)lds_plan(e->N, e->NL, e->E, e->F, e->block).bytes;
   P.world_size = e->cfg.world_size;
   const double pi = 3.141592653589793;
   P.pi = pi;
@@ -2446,6 +2641,7 @@ static void fill_params(const lsm_env* e, KParams& P) {
   P.o.masks = (float*)e->out_ptr[LSM_OUT_MASKS];
   P.o.active_masks = (float*)e->out_ptr[LSM_OUT_ACTIVE_MASKS];
   P.o.cforce = e->cfg.collision_forces ? (double*)e->out_ptr[LSM_OUT_COLLISION_FORCE] : nullptr;
+  P.o.departed = (uint8_t*)e->out_ptr[LSM_OUT_DEPARTED];
   P.stamps = (unsigned long long*)e->out_ptr[LSM_OUT_DEBUG_STAMPS];
   P.diag = 0;
 #ifdef LSM_STAMPS
@@ -2476,11 +2672,15 @@ size_t lsm_output_bytes(const lsm_env* e, int32_t slot) {
     case LSM_OUT_MASKS: return n * N * 4;
     case LSM_OUT_ACTIVE_MASKS: return n * N * 4;
     case LSM_OUT_COLLISION_FORCE: return n * N * 2 * 8;
+    case LSM_OUT_DEPARTED: return n * N;
     default: return 0;
   }
 }
 
 int32_t lsm_num_entities(const lsm_env* e) { return e->E; }
+int32_t lsm_layout_doubles(const lsm_env* e) {
+  return e ? 4 * e->N + 4 * e->NL + (e->cfg.scenario == LSM_SCENARIO_DEPARTURES ? 3 * e->N : 0) : 0;
+}
 int32_t lsm_node_features(const lsm_env* e) { return e->F; }
 int32_t lsm_obs_dim(const lsm_env* e) { return e->OBS; }
 const char* lsm_last_error(const lsm_env* e) { return e ? e->err.c_str() : "null handle"; }
@@ -2508,11 +2708,26 @@ int lsm_create(const lsm_config* cfg, lsm_env** out) {
   if (cfg->dynamics != LSM_DOUBLE_INTEGRATOR && cfg->dynamics != LSM_AIRTAXI)
     return fail(e, "dynamics must be LSM_DOUBLE_INTEGRATOR or LSM_AIRTAXI");
   if (N < 2 || N > BMAXN) return fail(e, "num_agents must be in [2, 64]");
-  if (L < 2 || L > MAX_L) return fail(e, "num_landmarks must be in [2, 8] (reference asserts > 1)");
+  if (L < (cfg->scenario == LSM_SCENARIO_TRAIN ? 2 : 1) || L > MAX_L)
+    return fail(e, "num_landmarks must be in [2, 8] (the training scenario asserts > 1, utils.py:31; "
+                   "layout scenarios: [1, 8])");
   if (N * (1 + L) > BMAXE) return fail(e, "N * (1 + L) must be <= 256");
   if (N * L - 1 > 127) return fail(e, "landmark ids go through np.int8 (navigation_graph_safe.py:581)");
   if (cfg->adj_layout != LSM_ADJ_REFERENCE && cfg->adj_layout != LSM_ADJ_COMPACT)
     return fail(e, "adj_layout must be LSM_ADJ_REFERENCE or LSM_ADJ_COMPACT");
+  if (cfg->scenario < LSM_SCENARIO_TRAIN || cfg->scenario > LSM_SCENARIO_DEPARTURES)
+    return fail(e, "scenario must be LSM_SCENARIO_TRAIN, _LAYOUT or _DEPARTURES");
+  if (cfg->rng != LSM_RNG_MT19937 && cfg->rng != LSM_RNG_PHILOX)
+    return fail(e, "rng must be LSM_RNG_MT19937 or LSM_RNG_PHILOX");
+  if (cfg->scenario != LSM_SCENARIO_TRAIN) {
+    if (cfg->auto_reset)
+      return fail(e, "layout scenarios are evaluation paths (GraphDummyVecEnv, scripts/eval_mpe.py): auto_reset must be 0");
+    if (N > MAXN || N * (1 + L) > MAXE) return fail(e, "layout scenarios need N <= 32 and N * (1 + L) <= 64");
+    if (cfg->rng != LSM_RNG_MT19937) return fail(e, "layout scenarios draw on the host: rng must be LSM_RNG_MT19937");
+  }
+  if (cfg->scenario == LSM_SCENARIO_DEPARTURES && cfg->dynamics != LSM_AIRTAXI)
+    return fail(e, "departure timers need airtaxi dynamics (RealisticScenario calls "
+                   "reset_velocity(theta, speed), KinematicVehicleXYState only, core.py:137)");
   {
     const char* kv = getenv("LSM_KERNEL");
     e->block = N > MAXN || N * (1 + L) > MAXE || (kv && strcmp(kv, "block") == 0);
@@ -2529,6 +2744,10 @@ int lsm_create(const lsm_config* cfg, lsm_env** out) {
   if (const char* v = getenv("LSM_LPE")) e->lpe = atoi(v);
   e->generic_only = getenv("LSM_GENERIC") && atoi(getenv("LSM_GENERIC")) != 0;
   if (e->block) e->lpe = 64;   // LSM_LPE applies to the one-wave kernel only
+  if (cfg->scenario != LSM_SCENARIO_TRAIN) {   // layouts: the generic one-wave kernel (mode 2 resets)
+    e->generic_only = true;
+    e->lpe = 64;
+  }
   // Team kernel (lsm_team.h) for the compile-time-N BASELINE agent counts: G envs per
   // workgroup share one wave for their per-agent phases. LSM_TEAM=0 selects rollout_kernel,
   // LSM_TEAM=G another instantiated G.
@@ -2558,7 +2777,15 @@ int lsm_create(const lsm_config* cfg, lsm_env** out) {
   r |= dalloc(e, &e->s.mt, n * MT_WORDS);
   r |= dalloc(e, &e->pairs, (size_t)e->E * (e->E - 1) / 2 + 1);
   r |= dalloc(e, &e->action_err, 1);
+  e->s.dep = nullptr;
+  if (cfg->scenario == LSM_SCENARIO_DEPARTURES) r |= dalloc(e, &e->s.dep, n * depw(N));
   if (r) return 1;
+  if (e->s.dep) {   // Agent.departed defaults to True (core.py:343), timers 0
+    std::vector<double> d(n * depw(N), 0.0);
+    for (size_t k = 0; k < n; ++k)
+      for (int i = 0; i < N; ++i) d[k * depw(N) + i] = 1.0;
+    HIPCHK(e, hipMemcpy(e->s.dep, d.data(), d.size() * 8, hipMemcpyHostToDevice));
+  }
   HIPCHK(e, hipMemset(e->action_err, 0, sizeof(int32_t)));
   {
     // agent-agent pairs first (the only ones needing the float64 blocks), then
@@ -2750,7 +2977,7 @@ int lsm_bind_output_ring(lsm_env* e, int32_t slot, void* base, size_t stride_byt
   if (!e) return 1;
   if (slot < 0 || slot >= LSM_NUM_OUT) return fail(e, "bad output slot");
   if (slot == LSM_OUT_RESET_FLAG || slot == LSM_OUT_EP_INFO || slot == LSM_OUT_EDGES ||
-      slot == LSM_OUT_DEBUG_STAMPS)
+      slot == LSM_OUT_DEBUG_STAMPS || slot == LSM_OUT_DEPARTED)
     return fail(e, "slot " + std::to_string(slot) + " cannot be ring-bound");
   if (count <= 0 || !base) {   // unbind
     e->ring_count[slot] = 0;
@@ -2873,6 +3100,7 @@ static int launch_block_t(lsm_env* e, const KStep& L, size_t env_lds, hipStream_
 static int launch(lsm_env* e, KStep& L, hipStream_t st) {
   size_t env_lds = lds_plan(e->N, e->NL, e->E, e->F, e->block).bytes;
   if (e->team) env_lds = team_env_bytes(env_lds, e->N);
+  if (e->cfg.scenario == LSM_SCENARIO_DEPARTURES) env_lds += dep_lds_bytes(e->N);
   if (e->block ? env_lds > 160 * 1024
                : (e->team ? env_lds * e->team > 160 * 1024 : env_lds * (WAVE / e->lpe) > 65536))
     return fail(e, "LDS footprint too large");
@@ -2951,6 +3179,27 @@ static int launch(lsm_env* e, KStep& L, hipStream_t st) {
   return 0;
 }
 
+// The kernel launch() dispatches to for this handle (same selection as launch()).
+const char* lsm_kernel_name(const lsm_env* e) {
+  static thread_local std::string name;
+  if (!e) return "";
+  const bool di = e->cfg.dynamics == LSM_DOUBLE_INTEGRATOR;
+  const int D = di ? 0 : 1;
+  if (e->block) {
+    const bool spec64 = e->N == 64 && e->L == 2 && !e->generic_only;
+    name = "rollout_block_kernel<" + std::to_string(D) + ", " + std::to_string(spec64 ? 64 : 0) + ">";
+  } else if (e->team) {
+    name = "rollout_team_kernel<" + std::to_string(D) + ", " + std::to_string(e->N) + ", " + std::to_string(e->team) + ">";
+  } else {
+    const bool specN = e->L == 2 && !e->generic_only &&
+                       ((e->lpe == 64 && ((di && (e->N == 3 || e->N == 8)) || (!di && (e->N == 3 || e->N == 16)))) ||
+                        (e->lpe == 32 && ((di && e->N == 8) || (!di && e->N == 16))));
+    name = "rollout_kernel<" + std::to_string(D) + ", " + std::to_string(e->lpe) + ", " +
+           std::to_string(specN ? e->N : 0) + ">";
+  }
+  return name.c_str();
+}
+
 int lsm_set_agent_state(lsm_env* e, int32_t env_index, const double* state, const int32_t* reached,
                         void* stream) {
   if (!e || !state) return 1;
@@ -2974,6 +3223,7 @@ int lsm_set_agent_state(lsm_env* e, int32_t env_index, const double* state, cons
 
 int lsm_reset(lsm_env* e, const lsm_curriculum* cur, void* stream) {
   if (!e || !cur) return 1;
+  if (e->cfg.scenario != LSM_SCENARIO_TRAIN) return fail(e, "layout scenario: reset with lsm_reset_layout");
   if (check_ready(e, false)) return 1;
   if (sep_check(e, cur)) return 1;
   KStep L;
@@ -2984,12 +3234,27 @@ int lsm_reset(lsm_env* e, const lsm_curriculum* cur, void* stream) {
   return launch(e, L, (hipStream_t)stream);
 }
 
+int lsm_reset_layout(lsm_env* e, const lsm_curriculum* cur, const double* layout, void* stream) {
+  if (!e || !cur) return 1;
+  if (e->cfg.scenario == LSM_SCENARIO_TRAIN) return fail(e, "lsm_reset_layout needs a layout scenario");
+  if (!layout) return fail(e, "null layout");
+  if (check_ready(e, false)) return 1;
+  if (sep_check(e, cur)) return 1;
+  KStep L;
+  memset(&L, 0, sizeof(L));
+  memcpy(L.cur_new, cur, sizeof(double) * NCUR);
+  L.mode = 2;
+  L.layout = layout;
+  return launch(e, L, (hipStream_t)stream);
+}
+
 int lsm_step(lsm_env* e, const void* actions, int32_t kind, const lsm_curriculum* cur, void* stream) {
   if (!e || !actions || !cur) return fail(e, "null argument");
   if (kind < 0 || kind > 2) return fail(e, "bad action kind");
   if (check_ready(e, true)) return 1;
   if (sep_check(e, cur)) return 1;
   KStep L;
+  memset(&L, 0, sizeof(L));
   memcpy(L.cur_new, cur, sizeof(double) * NCUR);
   L.mode = 0;
   L.action_kind = kind;
@@ -3016,6 +3281,19 @@ int lsm_host_rk45_di(const double* y0, double a0, double a1, double dt, double* 
 
 double lsm_host_glibc_pow(double x, double y) { return glibc_pow(x, y); }
 
+int lsm_host_philox4x32(const uint32_t* ctr, const uint32_t* key, uint32_t* out) {
+  philox4x32_10(ctr, key, out);
+  return 0;
+}
+
+int lsm_host_philox_uniforms(uint32_t key, uint32_t reset_index, int32_t count, double lo, double hi,
+                             double* out) {
+  Philox m;
+  m.init(key, reset_index);
+  for (int k = 0; k < count; ++k) out[k] = m.uniform(lo, hi);
+  return 0;
+}
+
 int lsm_host_mt_uniforms(uint32_t seed, int32_t count, double lo, double hi, double* out) {
   HostMT m;
   m.seed(seed);
@@ -3027,8 +3305,6 @@ int lsm_host_scenario(const lsm_config* cfg, const lsm_curriculum* cur, uint32_t
                       double* landmarks) {
   const int N = cfg->num_agents, L = cfg->num_landmarks, NL = N * L;
   if (N < 2 || N > BMAXN || L < 2 || L > MAX_L) return 1;
-  HostMT m;
-  m.seed(seed);
   ScenarioParams sp;
   const bool di = cfg->dynamics == LSM_DOUBLE_INTEGRATOR;
   sp.dyn = di ? 0 : 1; sp.N = N; sp.L = L; sp.world_size = cfg->world_size;
@@ -3038,7 +3314,15 @@ int lsm_host_scenario(const lsm_config* cfg, const lsm_curriculum* cur, uint32_t
   sp.ratio_airtaxi = cur->ratio_airtaxi; sp.ratio_scenario = cur->ratio_scenario;
   sp.pi = 3.141592653589793; sp.two_pi = 2 * sp.pi;
   std::vector<double> st(4 * N), lm(4 * NL), ws(SCEN_WS);
-  random_scenario(m, sp, st.data(), lm.data(), ws.data());
+  if (cfg->rng == LSM_RNG_PHILOX) {   // the device's first reset (reset index 0) of this seed
+    Philox m;
+    m.init(seed, 0);
+    random_scenario(m, sp, st.data(), lm.data(), ws.data());
+  } else {
+    HostMT m;
+    m.seed(seed);
+    random_scenario(m, sp, st.data(), lm.data(), ws.data());
+  }
   for (int i = 0; i < N; ++i)
     for (int c = 0; c < 4; ++c) agent_state[i * 4 + c] = st[c * N + i];
   for (int k = 0; k < NL; ++k)

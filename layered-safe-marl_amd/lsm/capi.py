@@ -17,8 +17,10 @@ LSM_DOUBLE_INTEGRATOR, LSM_AIRTAXI = 0, 1
 LSM_ACTIONS_INDEX_I32, LSM_ACTIONS_ONEHOT_F32, LSM_ACTIONS_ONEHOT_F64 = 0, 1, 2
 (OUT_OBS, OUT_NODE_OBS, OUT_ADJ, OUT_REWARD, OUT_DONE, OUT_RESET_FLAG, OUT_EP_INFO, OUT_INFO,
  OUT_EDGES, OUT_STATE, OUT_DEBUG_STAMPS, OUT_ADJ_MASK, OUT_SHARE_OBS, OUT_MASKS, OUT_ACTIVE_MASKS,
- OUT_COLLISION_FORCE) = range(16)
-NUM_OUT = 16
+ OUT_COLLISION_FORCE, OUT_DEPARTED) = range(17)
+NUM_OUT = 17
+LSM_SCENARIO_TRAIN, LSM_SCENARIO_LAYOUT, LSM_SCENARIO_DEPARTURES = 0, 1, 2
+LSM_RNG_MT19937, LSM_RNG_PHILOX = 0, 1
 ADJ_REFERENCE, ADJ_COMPACT = 0, 1
 INFO_FIELDS = ("individual_reward", "min_relative_distance", "Dist_to_goal", "Time_req_to_goal",
                "Num_agent_collisions", "Distance_mean", "Distance_variance", "Dists_traveled",
@@ -31,7 +33,9 @@ EXPORTED = ("lsm_create", "lsm_destroy", "lsm_last_error", "lsm_set_value_table"
             "lsm_node_features", "lsm_obs_dim", "lsm_host_mt_uniforms", "lsm_host_scenario",
             "lsm_set_agent_state", "lsm_edges_workspace_bytes", "lsm_edges_count", "lsm_edges_emit",
             "lsm_edges_last_error", "lsm_bind_output_ring", "lsm_select_ring", "lsm_buffer_insert",
-            "lsm_buffer_last_error", "lsm_host_rk45_di", "lsm_host_glibc_pow", "lsm_action_errors")
+            "lsm_buffer_last_error", "lsm_host_rk45_di", "lsm_host_glibc_pow", "lsm_action_errors",
+            "lsm_kernel_name", "lsm_reset_layout", "lsm_layout_doubles", "lsm_host_philox_uniforms",
+            "lsm_host_philox4x32")
 
 
 class LsmConfig(C.Structure):
@@ -40,7 +44,8 @@ class LsmConfig(C.Structure):
                 ("use_safety_filter", C.c_int32), ("use_masking", C.c_int32),
                 ("auto_reset", C.c_int32), ("emit_edges", C.c_int32), ("adj_layout", C.c_int32),
                 ("world_size", C.c_double), ("seed", C.c_int64), ("env_offset", C.c_int64),
-                ("collision_forces", C.c_int32), ("reserved0", C.c_int32)]
+                ("collision_forces", C.c_int32), ("scenario", C.c_int32), ("rng", C.c_int32),
+                ("reserved1", C.c_int32)]
 
 
 class LsmCurriculum(C.Structure):
@@ -94,6 +99,11 @@ def load_library(path: str = LIB_PATH):
         "lsm_host_rk45_di": (I32, [P, D, D, D, P]),
         "lsm_host_glibc_pow": (D, [D, D]),
         "lsm_action_errors": (I32, [P, P]),
+        "lsm_kernel_name": (C.c_char_p, [P]),
+        "lsm_reset_layout": (I32, [P, C.POINTER(LsmCurriculum), P, P]),
+        "lsm_layout_doubles": (I32, [P]),
+        "lsm_host_philox_uniforms": (I32, [U32, U32, I32, D, D, P]),
+        "lsm_host_philox4x32": (I32, [P, P, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

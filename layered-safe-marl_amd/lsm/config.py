@@ -82,6 +82,13 @@ ENTITY_SIZE = 0.050          # multiagent/core.py:261
 EPS_HJ = 0.4                 # multiagent/safety_filter.py:235,410
 
 
+# scenario_name values: the training scenario and the evaluation scenarios whose layouts
+# lsm.layouts restates (navigation_graph_safe_eval.py, navigation_graph_safe_bayarea_*.py)
+SCENARIOS = ("navigation_graph_safe", "navigation_graph_safe_eval", "navigation_graph_safe_bayarea_merge",
+             "navigation_graph_safe_bayarea_cross")
+EVAL_SCENARIO_TYPE = "left_to_right_merge_and_land"   # multiagent/config.py:86
+
+
 @dataclass
 class EnvArgs:
     """The env-side flags of ``all_args`` that the path reads."""
@@ -107,6 +114,10 @@ class EnvArgs:
     # RewardBinaryConfig.SEPARATION_DISTANCE_CURRICULUM (a hand-edited class constant in the
     # reference, config.py:81); None = that constant, True / False override it per env handle
     separation_distance_curriculum: Optional[bool] = None
+    # evaluation scenarios: multiagent.config.eval_scenario_type (a module constant in the
+    # reference) and the Bay Area map's (width, height) in pixels (the image is not in the reference)
+    eval_scenario_type: str = EVAL_SCENARIO_TYPE
+    bayarea_image_size: Optional[tuple] = None
 
     def sep_curriculum(self) -> bool:
         v = self.separation_distance_curriculum
@@ -127,8 +138,9 @@ class EnvArgs:
         return argparse.Namespace(**asdict(self))
 
     def validate(self):
-        if self.scenario_name not in ("navigation_graph_safe",):
-            raise ValueError("only the navigation_graph_safe training scenario is on the path")
+        if self.scenario_name not in SCENARIOS:
+            raise ValueError("scenario_name must be one of %s (the training scenario and its evaluation "
+                             "layouts, lsm.layouts)" % (SCENARIOS,))
         if self.num_obstacles != 0 or self.num_walls != 0 or self.num_scripted_agents != 0:
             raise ValueError("obstacles/walls/scripted agents are not supported by the graph mask "
                              "(navigation_graph_safe.py:976-989)")
@@ -136,7 +148,7 @@ class EnvArgs:
             raise ValueError("dynamics_type must be 'double_integrator' or 'airtaxi'")
         if self.graph_feat_type != "relative":
             raise ValueError("only graph_feat_type='relative' is on the path (train.sh)")
-        if self.num_landmarks < 1:
+        if self.num_landmarks < 1 and self.scenario_name == "navigation_graph_safe":
             raise ValueError("num_landmarks must be >= 1")
         if self.num_internal_step != 1:
             raise ValueError("num_internal_step != 1 is not supported")

@@ -19,7 +19,7 @@ import json
 import os
 import statistics
 
-KERNEL = "rollout_kernel"   # the one-wave kernel; --kernel rollout_block_kernel for N > 32
+KERNEL = "lsm::rollout"   # substring of every step-kernel variant (one-wave, team, workgroup)
 
 
 def _rows(d, suffix):

@@ -14,9 +14,13 @@ Mirrors the reference's vec-env surface for the navigation_graph_safe path
 All computation happens in ``liblsm_rollout.so`` (C ABI, HIP kernels). This
 class only allocates the device output buffers (torch tensors), computes the
 per-call curriculum block with the reference's float64 expressions, and converts
-outputs: ``return_numpy=True`` gives host numpy arrays like the reference
-(float32 instead of float64 for obs/node_obs/adj/rewards -- the runner's buffer
-stores float32); ``return_numpy=False`` keeps everything as device tensors.
+outputs: ``return_numpy=True`` gives host numpy arrays with the reference's dtypes
+(float64 obs/node_obs/adj/rewards holding the kernel's float32 values -- the runner's buffer
+stores float32 anyway); ``return_numpy=False`` keeps everything as device tensors.
+
+Evaluation scenarios (``layout=lsm.layouts.ScenarioLayout(...)``): the reset's layout is
+computed on the host from each env's numpy stream and handed to ``lsm_reset_layout``; every
+step (and, for the Bay Area maps, the departure timers) runs on the device.
 """
 from __future__ import annotations
 
@@ -29,6 +33,8 @@ from . import capi
 from .config import EnvArgs
 from .curriculum import curriculum_block, to_struct
 from .hj_tables import HjTable, default_tables
+from .layouts import ScenarioLayout
+from .share_vec_env import ShareVecEnv
 from .spaces import Box, Discrete
 
 EPKEYS = ("travel_time_mean", "travel_distance_mean", "done_percentage", "num_reached_goal_mean",
@@ -44,7 +50,7 @@ class EnvInfos(list):
     """Per-env info list built lazily from the device info tensor (host copy)."""
 
 
-def infos_from_arrays(info, reset, ep_info, auto_reset=True):
+def infos_from_arrays(info, reset, ep_info, auto_reset=True, departed=None):
     """The reference's per-env info lists from the device arrays: per agent the
     ``info_callback`` dict (navigation_graph_safe.py:386-450) plus the keys
     ``MultiAgentGraphEnv.step`` adds (environment.py:1025-1029), then the episode summary as
@@ -68,7 +74,7 @@ def infos_from_arrays(info, reset, ep_info, auto_reset=True):
             d["Mean_by_variance"] = d["Distance_mean"] / (d["Distance_variance"] + 0.0001)
             d["Time_taken"] = d["Time_req_to_goal"]
             d["Time_mean_by_stddev"] = d["Time_mean"] / (d["Time_stddev"] + 0.0001)
-            d["Departed"] = True
+            d["Departed"] = True if departed is None else bool(departed[e, i])
             lst.append(d)
         if auto_reset and reset[e]:
             lst.append({k: float(ep_info[e, j]) for j, k in enumerate(EPKEYS)})
@@ -89,18 +95,35 @@ def expand_compact_adj(adj, mask, E):
     return torch.where(keep, adj.unsqueeze(1), torch.zeros((), dtype=adj.dtype, device=adj.device))
 
 
-class GpuGraphVecEnv:
+class GpuGraphVecEnv(ShareVecEnv):
+    """rng: "mt19937" (the reference's draws, default) or "philox" (fast device resets, same
+    scenario distribution). layout: an evaluation ScenarioLayout (needs auto_reset=False)."""
+
     def __init__(self, all_args, num_envs: Optional[int] = None, device=None,
                  value_table: Optional[HjTable] = None, ttr_table: Optional[HjTable] = None,
                  auto_reset: bool = True, env_offset: int = 0, emit_edges: bool = False,
                  return_numpy: bool = True, build_infos: bool = True, small_tables: bool = False,
-                 adj_layout: str = "reference", collision_forces: bool = False):
+                 adj_layout: str = "reference", collision_forces: bool = False,
+                 layout: Optional[ScenarioLayout] = None, rng: str = "mt19937"):
         torch = _torch()
         self.args = EnvArgs.from_namespace(all_args) if not isinstance(all_args, EnvArgs) else all_args
         self.args.validate()
         a = self.args
-        if a.num_landmarks < 2:
+        if layout is None and a.scenario_name != "navigation_graph_safe":
+            from .layouts import from_args
+            layout = from_args(a)
+        self.layout = layout
+        if layout is not None:
+            if auto_reset:
+                raise ValueError("evaluation layouts run with GraphDummyVecEnv semantics (auto_reset=False), "
+                                 "as scripts/eval_mpe.py does")
+            if layout.N != int(a.num_agents):
+                raise ValueError("layout built for %d agents, args.num_agents = %d" % (layout.N, a.num_agents))
+            a.num_landmarks = layout.L
+        elif a.num_landmarks < 2:
             raise ValueError("num_landmarks must be >= 2 (reference asserts, utils.py:31)")
+        if rng not in ("mt19937", "philox"):
+            raise ValueError("rng must be 'mt19937' or 'philox'")
         self.num_envs = int(num_envs if num_envs is not None else a.n_rollout_threads)
         self.device = torch.device(device if device is not None else "cuda:%d" % torch.cuda.current_device())
         if self.device.type != "cuda":
@@ -123,7 +146,9 @@ class GpuGraphVecEnv:
                              adj_layout=capi.ADJ_COMPACT if adj_layout == "compact" else capi.ADJ_REFERENCE,
                              world_size=float(a.world_size),
                              seed=int(a.seed), env_offset=int(env_offset),
-                             collision_forces=int(bool(collision_forces)))
+                             collision_forces=int(bool(collision_forces)),
+                             scenario=layout.scenario_code if layout is not None else capi.LSM_SCENARIO_TRAIN,
+                             rng=capi.LSM_RNG_PHILOX if rng == "philox" else capi.LSM_RNG_MT19937)
         if int(a.seed) + 1000 * (int(env_offset) + self.num_envs - 1) >= 2 ** 32:
             raise ValueError("numpy seeds must be < 2**32 (seed + 1000 * env index)")
         h = C.c_void_p()
@@ -166,12 +191,16 @@ class GpuGraphVecEnv:
         self.t_edges = torch.zeros((n, E, E), dtype=torch.uint8, device=dev) if emit_edges else None
         # World.get_entity_collision_force per agent (optional report; never applied, like the reference)
         self.t_cforce = torch.zeros((n, N, 2), dtype=torch.float64, device=dev) if collision_forces else None
+        # info 'Departed' (RealisticScenario departure timers)
+        self.t_departed = (torch.zeros((n, N), dtype=torch.bool, device=dev)
+                           if layout is not None and layout.departures else None)
         for slot, t in ((capi.OUT_OBS, self.t_obs), (capi.OUT_NODE_OBS, self.t_node),
                         (capi.OUT_ADJ, self.t_adj), (capi.OUT_REWARD, self.t_rew),
                         (capi.OUT_DONE, self.t_done), (capi.OUT_RESET_FLAG, self.t_reset),
                         (capi.OUT_EP_INFO, self.t_epinfo), (capi.OUT_INFO, self.t_info),
                         (capi.OUT_STATE, self.t_state), (capi.OUT_EDGES, self.t_edges),
-                        (capi.OUT_ADJ_MASK, self.t_adj_mask), (capi.OUT_COLLISION_FORCE, self.t_cforce)):
+                        (capi.OUT_ADJ_MASK, self.t_adj_mask), (capi.OUT_COLLISION_FORCE, self.t_cforce),
+                        (capi.OUT_DEPARTED, self.t_departed)):
             if t is None:
                 continue
             capi.check(self.lib.lsm_bind_output(h, slot, C.c_void_p(t.data_ptr()),
@@ -190,6 +219,11 @@ class GpuGraphVecEnv:
         self._cur_cache = {}
         self._last_ep = 0
         self.closed = False
+        # evaluation layouts draw from each env's numpy stream on the host (np.random.seed(seed +
+        # 1000 k) after make_world, MPE_env.py:56-84)
+        self._rngs = ([np.random.RandomState(int(a.seed) + 1000 * (int(env_offset) + k)) for k in range(n)]
+                      if layout is not None else None)
+        self.kernel_name = self.lib.lsm_kernel_name(h).decode()
 
     # -- tables ------------------------------------------------------------------------
     def _set_table(self, fn, t: HjTable, values, grads, extra=()):
@@ -222,12 +256,26 @@ class GpuGraphVecEnv:
         block = curriculum_block(self.args, num_current_episode)
         self._last_ep = num_current_episode
         cur = to_struct(block)
-        capi.check(self.lib.lsm_reset(self.h, C.byref(cur), self._stream()), self.h)
+        if self.layout is None:
+            capi.check(self.lib.lsm_reset(self.h, C.byref(cur), self._stream()), self.h)
+        else:
+            torch = _torch()
+            prev = self.t_state.cpu().numpy()
+            lay = np.stack([self.layout.draw(self._rngs[k], prev[k]).pack() for k in range(self.num_envs)])
+            assert lay.shape[1] == self.lib.lsm_layout_doubles(self.h)
+            self._layout_dev = torch.as_tensor(lay, dtype=torch.float64, device=self.device).contiguous()
+            capi.check(self.lib.lsm_reset_layout(self.h, C.byref(cur), C.c_void_p(self._layout_dev.data_ptr()),
+                                                 self._stream()), self.h)
         ep = self._ep_info_all()
         if self.return_numpy:
-            return (self.t_obs.cpu().numpy(), self.agent_id.cpu().numpy(), self.t_node.cpu().numpy(),
-                    self.reference_adj().cpu().numpy(), ep)
+            return (self._host64(self.t_obs), self.agent_id.cpu().numpy(), self._host64(self.t_node),
+                    self._host64(self.reference_adj()), ep)
         return self.t_obs, self.agent_id, self.t_node, self.t_adj, ep
+
+    @staticmethod
+    def _host64(t):
+        """Host copy with the reference's float64 dtype (values are the kernel's float32 ones)."""
+        return t.cpu().numpy().astype(np.float64)
 
     def _ep_info_all(self):
         e = self.t_epinfo.cpu().numpy()
@@ -272,10 +320,10 @@ class GpuGraphVecEnv:
                    (self.t_info, self.t_reset, self.t_epinfo))
             return out + (0,) if not self.auto_reset else out
         self.check_actions()   # the host copies below synchronise anyway
-        obs = self.t_obs.cpu().numpy()
-        node = self.t_node.cpu().numpy()
-        adj = self.reference_adj().cpu().numpy()
-        rew = self.t_rew.cpu().numpy()
+        obs = self._host64(self.t_obs)
+        node = self._host64(self.t_node)
+        adj = self._host64(self.reference_adj())
+        rew = self._host64(self.t_rew)
         dones = self.t_done.cpu().numpy().astype(bool)
         infos = self._infos() if self.build_infos else None
         aid = self.agent_id.cpu().numpy()
@@ -299,7 +347,8 @@ class GpuGraphVecEnv:
     def _infos(self):
         reset = self.t_reset.cpu().numpy()
         return infos_from_arrays(self.t_info.cpu().numpy(), reset,
-                                 self.t_epinfo.cpu().numpy() if reset.any() else None, self.auto_reset)
+                                 self.t_epinfo.cpu().numpy() if reset.any() else None, self.auto_reset,
+                                 None if self.t_departed is None else self.t_departed.cpu().numpy())
 
     def reference_adj(self):
         """The adjacency in the reference layout [n, N, E, E] (device tensor). In the compact
@@ -328,6 +377,9 @@ class GpuGraphVecEnv:
     def state(self):
         """Agent states [n, N, 4] (float64) after the last call (positions/velocities)."""
         return self.t_state
+
+    def close_extras(self):
+        self.close()
 
     def close(self):
         if not self.closed and getattr(self, "h", None):

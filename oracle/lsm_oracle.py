@@ -234,6 +234,10 @@ class OracleEnv:
         self.atime = np.zeros(self.N)
         self.done = np.zeros(self.N, dtype=bool)
         self.departed = np.ones(self.N, dtype=bool)
+        # RealisticScenario (navigation_graph_safe.py:1124-1186): departure timers and init headings
+        self.realistic = False
+        self.departure_timer = np.zeros(self.N)
+        self.init_theta = np.zeros(self.N)
         self.lm_pos = np.zeros((self.NL, 2))
         self.lm_heading = np.zeros(self.NL)
         self.lm_speed = np.zeros(self.NL)
@@ -468,7 +472,10 @@ class OracleEnv:
         self.edge_list = np.stack([row, col])
         return self.edge_list
 
-    def reset(self, num_current_episode=0):
+    def reset(self, num_current_episode=0, layout=None):
+        """MultiAgentGraphEnv.reset (environment.py:1046-1074). layout: an evaluation Scenario's
+        random_scenario result (lsm.layouts.Layout: state, landmarks, and for RealisticScenario
+        departed / timer / init_theta), set as the reference's layout functions set the world."""
         self._reached_at_reset = self.reached_goal.copy()
         self.current_step = 0
         self.current_time_step = 0
@@ -476,7 +483,20 @@ class OracleEnv:
         self.p_dist[:] = 0.0
         self.atime[:] = 0.0
         self.update_curriculum(num_current_episode)
-        self.random_scenario()
+        if layout is None:
+            self.random_scenario()
+        else:
+            self.s[:] = layout.state
+            self.lm_pos[:] = layout.landmarks[:, :2]
+            self.lm_heading[:] = layout.landmarks[:, 2]
+            self.lm_speed[:] = layout.landmarks[:, 3]
+            if layout.clears_done:
+                self.done[:] = False
+            if layout.departed is not None:
+                self.realistic = True
+                self.departed[:] = layout.departed.astype(bool)
+                self.departure_timer[:] = layout.timer
+                self.init_theta[:] = layout.init_theta
         for i in range(self.N):
             self.goal_min_time[i] = np.sqrt(np.sum(np.square(self.pos(i) - self.lm_pos[i]))) / self.max_speed
         self.calculate_distances()
@@ -625,8 +645,33 @@ class OracleEnv:
                 rew -= sen * cra
         return rew
 
+    def _realistic_update(self, i):
+        """RealisticScenario.update_reached_goal_and_done (navigation_graph_safe.py:1153-1186)."""
+        if self.departure_timer[i] <= 0 and not self.departed[i]:
+            if self.min_rel_dist[i] > self.sep_target:
+                self.s[i, 2] = self.init_theta[i]       # reset_velocity(theta=init_theta,
+                self.s[i, 3] = self.goal_speed_max      #                speed=goal_speed_max)
+                self.departed[i] = True
+        elif not self.departed[i]:
+            self.departure_timer[i] -= 1
+            self.s[i, 3] = 0.0                          # freeze_agent (airtaxi)
+        if self.goal_reached(i):
+            if self.use_masking:
+                if not self.done[i]:
+                    self.reached_goal[i] += 1
+            else:
+                self.reached_goal[i] += 1
+            if self.reached_goal[i] >= self.L:
+                self.done[i] = True
+                self.s[i, 3] = 0.0
+            else:
+                self._realistic_update(i)
+
     def reward(self, i):
         rew = self.reward_reach_goal(i)
+        if self.realistic:
+            self._realistic_update(i)
+            return np.clip(rew, MIN_REWARD, MAX_REWARD)
         if self.goal_reached(i):
             if self.use_masking:
                 if not self.done[i]:
@@ -1038,8 +1083,9 @@ class OracleVecEnv:
                      for k in range(n_envs)]
         self.auto_reset = auto_reset
 
-    def reset(self, ep=0):
-        res = [e.reset(ep) for e in self.envs]
+    def reset(self, ep=0, layouts=None):
+        """layouts: per-env evaluation layouts (lsm.layouts.Layout) or None (training scenario)."""
+        res = [e.reset(ep, None if layouts is None else layouts[k]) for k, e in enumerate(self.envs)]
         obs, aid, node, adj, info = zip(*res)
         return (np.stack([np.array(o) for o in obs]), np.stack([np.array(a) for a in aid]),
                 np.stack([np.array(n) for n in node]), np.stack([np.array(a) for a in adj]), info)

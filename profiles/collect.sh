@@ -14,8 +14,9 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 BENCH="bench.py --config $CFG --steps 200 --warmup 20 --no-cpu-baseline"
 ENVS=$(python -c "import bench; print(bench.CONFIGS[$CFG]['envs'])")
-KERN=rollout_kernel
-if [ "$CFG" = "5" ]; then KERN=rollout_block_kernel; fi
+# the step kernel of any variant (rollout_kernel / rollout_team_kernel / rollout_block_kernel);
+# bench.py's line names the instantiation (lsm_kernel_name)
+KERN="lsm::rollout"
 
 run() {  # run <name> <rocprofv3 args...>
   local name=$1; shift

@@ -58,14 +58,36 @@ def pack_adj(adj_list):
     return np.packbits(nz.reshape(-1))
 
 
+def _dep_rows(world):
+    """departed, departure_timer, state.init_theta per agent (RealisticScenario; defaults else)."""
+    return np.array([[float(a.departed), float(getattr(a, "departure_timer", 0)),
+                      float(getattr(a.state, "init_theta", 0.0) or 0.0)] for a in world.agents])
+
+
 def run_case(name, args, seed, ep, steps, value_stored=None, ttr_stored=None, inject=None,
-             action_seed=0, runner_episodes=False, sep_curriculum=False):
+             action_seed=0, runner_episodes=False, sep_curriculum=False, eval_type=None, image_size=None,
+             dummy=False):
     """runner_episodes: step t passes the runner's episode counter ep + t // episode_length, as
     GMPERunner.run does (graph_mpe_runner.py:72-103), so the worker's auto-resets
     (env_wrappers.py:866-871) move through the curriculum. sep_curriculum: the reference's
     RewardBinaryConfig.SEPARATION_DISTANCE_CURRICULUM (config.py:81) set while the env is made
-    (make_world reads it, navigation_graph_safe.py:183-191)."""
+    (make_world reads it, navigation_graph_safe.py:183-191). eval_type: multiagent.config.
+    eval_scenario_type for the navigation_graph_safe_eval Scenario (read when the scenario module is
+    loaded). image_size: (w, h) of a blank map image written where RealisticScenario opens it (the
+    Bay Area images are not in the reference; only their size is read). dummy: GraphDummyVecEnv
+    semantics (no auto-reset; the render loop resets after every episode_length steps)."""
     work = tempfile.mkdtemp(prefix="lsm_ref_")
+    ref_harness._install_paths()
+    import multiagent.config as mconfig
+    old_type = mconfig.eval_scenario_type
+    if eval_type is not None:
+        mconfig.eval_scenario_type = eval_type
+    if image_size is not None:
+        from PIL import Image
+        d = os.path.join(work, "multiagent", "custom_scenarios", "data")
+        os.makedirs(d, exist_ok=True)
+        fname = args.scenario_name.replace("navigation_graph_safe_", "") + ".jpg"
+        Image.new("RGB", tuple(image_size)).save(os.path.join(d, fname))
     di = args.dynamics_type == "double_integrator"
     if value_stored is not None or ttr_stored is not None:
         ref_harness.write_data_files(work, di_table=value_stored if di else None,
@@ -80,12 +102,14 @@ def run_case(name, args, seed, ep, steps, value_stored=None, ttr_stored=None, in
             RewardBinaryConfig.SEPARATION_DISTANCE_CURRICULUM = old
     else:
         env = ref_harness.make_reference_env(args, work, seed)
+    mconfig.eval_scenario_type = old_type
     scen = env.reward_callback.__self__
     world = env.world
     N = args.num_agents
     rng = np.random.default_rng(action_seed)
     rec = {k: [] for k in ("act", "state", "reached", "done", "dones", "rew", "obs", "adj_bits",
-                           "minrel", "sfilt", "decon", "edges_n", "info_num", "ptime", "step_ep", "hj_sep")}
+                           "minrel", "sfilt", "decon", "edges_n", "info_num", "ptime", "step_ep", "hj_sep",
+                           "departed")}
     full = {}
     resets = []
 
@@ -105,6 +129,7 @@ def run_case(name, args, seed, ep, steps, value_stored=None, ttr_stored=None, in
     full["reset0_lm"] = np.array([[l.state.p_pos[0], l.state.p_pos[1], l.heading, l.speed]
                                   for l in world.landmarks])
     full["reset0_edges"] = np.array(world.edge_list)
+    full["reset0_dep"] = _dep_rows(world)
     if inject is not None:
         inject(world, scen)
         full["inject_state"] = np.array([a.state.values for a in world.agents])
@@ -134,12 +159,13 @@ def run_case(name, args, seed, ep, steps, value_stored=None, ttr_stored=None, in
         rec["step_ep"].append(ep_t)
         hj = world.hj_data_handle
         rec["hj_sep"].append(float(hj.separation_distance) if hj is not None else np.nan)
+        rec["departed"].append(np.array([a.departed for a in world.agents]))
         changed = t > 0 and not np.array_equal(rec["done"][-1], rec["done"][-2])
         if t in FULL_STEPS or t % 50 == 0 or changed:
             full["t%03d_node" % t] = np.array(node, dtype=np.float32)
             full["t%03d_adj" % t] = np.array(adj, dtype=np.float32)
             full["t%03d_edges" % t] = edges
-        if np.all(done_n):
+        if (np.all(done_n) and not dummy) or (dummy and (t + 1) % args.episode_length == 0):
             r = ref_harness.run_in(work, env.reset, ep_t)
             obs, aid, node, adj, epinfo = r
             resets.append((t + 1, [epinfo[k] for k in EPKEYS]))
@@ -147,6 +173,7 @@ def run_case(name, args, seed, ep, steps, value_stored=None, ttr_stored=None, in
             full["t%03d_reset_state" % t] = np.array([a.state.values for a in world.agents])
             full["t%03d_reset_lm" % t] = np.array(
                 [[l.state.p_pos[0], l.state.p_pos[1], l.heading, l.speed] for l in world.landmarks])
+            full["t%03d_reset_dep" % t] = _dep_rows(world)
             full["t%03d_reset_node" % t] = np.array(node, dtype=np.float32)
             full["t%03d_reset_adj" % t] = np.array(adj, dtype=np.float32)
     out = {k: np.array(v) for k, v in rec.items()}
@@ -156,6 +183,11 @@ def run_case(name, args, seed, ep, steps, value_stored=None, ttr_stored=None, in
     meta = dict(vars(args)); meta.update(name=name, env_seed=seed, ep=ep, steps=steps)
     if sep_curriculum:
         meta["separation_distance_curriculum"] = True
+    if eval_type is not None:
+        meta["eval_scenario_type"] = eval_type
+    if image_size is not None:
+        meta["bayarea_image_size"] = tuple(image_size)
+    meta["dummy"] = bool(dummy)
     out["meta"] = np.array(repr(meta))
     path = os.path.join(HERE, name + ".npz")
     np.savez_compressed(path, **out)
@@ -271,6 +303,46 @@ def main(only=None):
                          seed=23, ep=3, steps=200, value_stored=at_small, ttr_stored=ttr_small,
                          action_seed=9, runner_episodes=True, sep_curriculum=True),
     ]
+    # evaluation layouts (navigation_graph_safe_eval.py) and the RealisticScenario Bay Area maps
+    # with departure timers (navigation_graph_safe.py:1124-1186), GraphDummyVecEnv semantics
+    layouts = [
+        lambda: run_case("ev_di_lrmland_n4", A(scenario_name="navigation_graph_safe_eval", num_agents=4,
+                                               num_landmarks=0, num_env_steps=80 * 4, episode_length=80,
+                                               use_safety_filter=True),
+                         seed=31, ep=4, steps=160, value_stored=di_small, action_seed=10,
+                         eval_type="left_to_right_merge_and_land", dummy=True),
+        lambda: run_case("ev_di_btmland_n3", A(scenario_name="navigation_graph_safe_eval", num_agents=3,
+                                               num_landmarks=0, num_env_steps=60 * 4, episode_length=60),
+                         seed=32, ep=1, steps=120, action_seed=11, eval_type="bottom_to_top_merge_and_land",
+                         dummy=True),
+        lambda: run_case("ev_at_circ_n4", A(scenario_name="navigation_graph_safe_eval", num_agents=4,
+                                            num_landmarks=0, num_env_steps=120 * 4, dynamics_type="airtaxi",
+                                            world_size=6, episode_length=120, use_safety_filter=True),
+                         seed=33, ep=4, steps=120, value_stored=at_small, ttr_stored=ttr_small,
+                         action_seed=12, eval_type="circular_config", dummy=True),
+        lambda: run_case("ev_at_conflict3", A(scenario_name="navigation_graph_safe_eval", num_agents=3,
+                                              num_landmarks=0, num_env_steps=80 * 4, dynamics_type="airtaxi",
+                                              world_size=6, episode_length=80, use_safety_filter=True),
+                         seed=34, ep=4, steps=80, value_stored=at_small, ttr_stored=ttr_small,
+                         action_seed=13, eval_type="three_vehicle_conflicting_example", dummy=True),
+        lambda: run_case("ba_merge_n8", A(scenario_name="navigation_graph_safe_bayarea_merge", num_agents=8,
+                                          num_landmarks=0, num_env_steps=150 * 4, dynamics_type="airtaxi",
+                                          episode_length=150, use_safety_filter=True),
+                         seed=35, ep=4, steps=150, value_stored=at_small, ttr_stored=ttr_small,
+                         action_seed=14, image_size=(2400, 2000), dummy=True),
+        lambda: run_case("ba_cross_n4", A(scenario_name="navigation_graph_safe_bayarea_cross", num_agents=4,
+                                          num_landmarks=0, num_env_steps=380 * 4, dynamics_type="airtaxi",
+                                          episode_length=380, use_safety_filter=True),
+                         seed=36, ep=4, steps=380, value_stored=at_small, ttr_stored=ttr_small,
+                         action_seed=15, image_size=(3300, 3000), dummy=True),
+    ]
+    if only == "layouts":
+        for f in layouts:
+            f()
+        return
+    if only == "ba_cross":
+        layouts[-1]()
+        return
     if only == "collision":
         record_collision_forces()
         return

@@ -120,3 +120,66 @@ def test_header_is_plain_c_abi():
         if shutil.which(cc) is None:
             pytest.skip("%s not available" % cc)
         subprocess.check_call([cc, std, "-Wall", "-Wextra", "-Werror", "-fsyntax-only", "-x", lang, hdr])
+
+
+# ---- Philox fast-reset stream (LSM_RNG_PHILOX) ---------------------------------------------------
+# Random123 known-answer vectors for philox4x32_R(10, ctr, key) (kat_vectors: ctr, key, expected)
+PHILOX_KAT = [
+    ((0, 0, 0, 0), (0, 0), (0x6627E8D5, 0xE169C58D, 0xBC57AC4C, 0x9B00DBD8)),
+    ((0xFFFFFFFF,) * 4, (0xFFFFFFFF,) * 2, (0x408F276D, 0x41C83B0E, 0xA20BC7C6, 0x6D5451FD)),
+    ((0x243F6A88, 0x85A308D3, 0x13198A2E, 0x03707344), (0xA4093822, 0x299F31D0),
+     (0xD16CFE09, 0x94FDCCEB, 0x5001E420, 0x24126EA1)),
+]
+
+
+@pytest.mark.parametrize("ctr,key,want", PHILOX_KAT)
+def test_philox_known_answers(lib, ctr, key, want):
+    c = np.array(ctr, dtype=np.uint32)
+    k = np.array(key, dtype=np.uint32)
+    out = np.zeros(4, dtype=np.uint32)
+    assert lib.lsm_host_philox4x32(c.ctypes.data, k.ctypes.data, out.ctypes.data) == 0
+    assert tuple(int(x) for x in out) == want
+
+
+def test_philox_uniforms_are_uniform_and_counter_based(lib):
+    n = 200000
+    a = np.zeros(n)
+    b = np.zeros(n)
+    lib.lsm_host_philox_uniforms(12345, 0, n, -2.0, 3.0, a.ctypes.data)
+    lib.lsm_host_philox_uniforms(12345, 1, n, -2.0, 3.0, b.ctypes.data)
+    assert a.min() >= -2.0 and a.max() < 3.0
+    assert abs(a.mean() - 0.5) < 0.02 and abs(a.std() - 5 / np.sqrt(12)) < 0.02
+    hist = np.histogram(a, bins=20, range=(-2, 3))[0]
+    assert hist.min() > 0.9 * n / 20 and hist.max() < 1.1 * n / 20
+    assert not np.array_equal(a[:100], b[:100])          # another reset index, another stream
+    c = np.zeros(100)
+    lib.lsm_host_philox_uniforms(12345, 0, 100, -2.0, 3.0, c.ctypes.data)
+    np.testing.assert_array_equal(a[:100], c)             # same (key, reset) -> same draws
+
+
+@pytest.mark.parametrize("dyn,n", [("double_integrator", 8), ("airtaxi", 16)])
+def test_host_scenario_philox_distribution(lib, dyn, n):
+    """The fast mode draws the same scenario distribution: agents / goals in the reference's
+    boxes, goals separated as randomly_generate_separated_positions requires (utils.py:39-68)."""
+    ws = 4 if dyn == "double_integrator" else 6
+    cfg = capi.LsmConfig(dynamics=0 if dyn == "double_integrator" else 1, num_envs=1, num_agents=n,
+                         num_landmarks=2, episode_length=250, world_size=ws, rng=capi.LSM_RNG_PHILOX)
+    args = EnvArgs(dynamics_type=dyn, num_agents=n, world_size=ws, num_env_steps=250 * 4, use_safety_filter=True)
+    cur = curriculum.to_struct(curriculum.curriculum_block(args, 4))
+    seen = []
+    for seed in range(40):
+        st = np.zeros((n, 4))
+        lm = np.zeros((2 * n, 4))
+        assert lib.lsm_host_scenario(cfg, cur, seed * 1000 + 7, st.ctypes.data, lm.ctypes.data) == 0
+        if dyn == "double_integrator":
+            assert np.all(np.abs(st[:, :2]) <= 0.8 * ws) and np.all(st[:, 2:] == 0)
+            dmin, dmax = 0.25 * 4.0, 0.75 * 4.0
+        else:
+            assert np.all(st[:, 0] >= -0.5 * ws) and np.all(st[:, 0] <= 0.25 * ws)
+            assert np.all(np.abs(st[:, 1]) <= 0.5 * ws) and np.all((st[:, 2] >= 0) & (st[:, 2] < 2 * np.pi))
+            dmin, dmax = 0.5 * 3 * 1.60934, 3 * 1.60934
+        # agent 0's two goals (later agents may reuse the previous agent's goals, :1296-1300)
+        seen.append(np.linalg.norm(lm[0, :2] - lm[n, :2]))
+    d = np.array(seen)
+    # the separation draw retries up to 1000 times: essentially every pair satisfies it
+    assert np.mean((d > dmin) & (d < dmax)) > 0.95

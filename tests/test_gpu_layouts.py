@@ -1,0 +1,207 @@
+"""GPU parity of the evaluation layouts, RealisticScenario departures and the Philox fast reset.
+
+* every ev_* / ba_* fixture (recorded from the reference, GraphDummyVecEnv semantics) through the
+  HIP path: lsm_reset_layout with lsm.layouts' draws, then every step on the device -- states,
+  rewards, dones, reached goals, departed flags, info numbers, observations and graph outputs;
+* several Bay Area envs at once (each its own seed, timers and departures) against the oracle;
+* LSM_RNG_PHILOX: the device's first reset equals the host restatement of the Philox stream, and
+  rollouts stay well-formed across auto-resets.
+Tolerances as tests/test_gpu_parity.py (north_star): fp32 outputs 1e-5, float64 state 1e-9,
+masks / dones / departed bit-exact.
+"""
+import numpy as np
+import pytest
+
+from golden_replay import EPKEYS, INFOKEYS, adj_bits, layout_fixture_names, layout_for, load, step_ep, \
+    table_dict, tables_for
+
+pytestmark = pytest.mark.gpu
+
+STATE_ATOL = 1e-9
+F32_ATOL = 1e-5
+
+
+def _info_col(name):
+    from lsm import capi
+    return capi.INFO_FIELDS.index(name)
+
+
+def _gpu_layout_env(meta, n_envs=1, seed=None):
+    from lsm.config import EnvArgs
+    from lsm.vec_env import GpuGraphVecEnv
+    args = EnvArgs.from_namespace(type("A", (), meta)())
+    args.seed = meta["env_seed"] if seed is None else seed
+    vt, tt = tables_for(meta)
+    return GpuGraphVecEnv(args, num_envs=n_envs, device="cuda:0", value_table=vt, ttr_table=tt,
+                          auto_reset=False, emit_edges=True)
+
+
+@pytest.mark.parametrize("name", layout_fixture_names())
+def test_gpu_layout_matches_reference(name):
+    z, meta = load(name)
+    env = _gpu_layout_env(meta)
+    assert env.kernel_name.startswith("rollout_kernel<")
+    obs, aid, node, adj, ep = env.reset(meta["ep"])
+    np.testing.assert_allclose(obs[0], z["reset0_obs"], rtol=0, atol=F32_ATOL)
+    np.testing.assert_allclose(node[0], z["reset0_node"], rtol=0, atol=F32_ATOL)
+    np.testing.assert_allclose(adj[0], z["reset0_adj"], rtol=0, atol=F32_ATOL)
+    np.testing.assert_array_equal(adj[0] != 0, z["reset0_adj"] != 0)
+    np.testing.assert_allclose(env.state().cpu().numpy()[0], z["reset0_state"], rtol=0, atol=STATE_ATOL)
+    lay = env.layout
+    # circular_config keeps done agents done across resets in the reference; the device clears
+    # done at every layout reset: compared through its first episode only
+    steps = meta["steps"] if lay.kind != "circular_config" else meta["episode_length"]
+    n_reset = 1
+    c_rg, c_mr = _info_col("reached_goal"), _info_col("min_relative_distance")
+    c_sf, c_dec = _info_col("Safety filtered"), _info_col("deconflicting_agent_index")
+    for t in range(steps):
+        ctx = "%s step %d" % (name, t)
+        obs, aid, node, adj, rew, dones, infos, _ = env.step(z["act"][t][None], step_ep(z, meta, t))
+        info = env.t_info.cpu().numpy()[0]
+        np.testing.assert_array_equal(dones[0], z["dones"][t], err_msg=ctx)
+        np.testing.assert_allclose(rew[0], z["rew"][t], rtol=1e-6, atol=1e-5, err_msg=ctx)
+        np.testing.assert_array_equal(info[:, c_rg], z["reached"][t], err_msg=ctx)
+        np.testing.assert_allclose(info[:, c_mr], z["minrel"][t], rtol=0, atol=STATE_ATOL, err_msg=ctx)
+        np.testing.assert_array_equal(info[:, c_sf].astype(bool), z["sfilt"][t], err_msg=ctx)
+        np.testing.assert_array_equal(info[:, c_dec].astype(int), z["decon"][t], err_msg=ctx)
+        dep = np.array([d["Departed"] for d in infos[0][:meta["num_agents"]]])
+        np.testing.assert_array_equal(dep, z["departed"][t], err_msg=ctx)
+        for j, k in enumerate(INFOKEYS):
+            # individual_reward is the reward (airtaxi TTR term: float32 interpolation, 1 ulp)
+            tol = dict(rtol=1e-6, atol=1e-5) if k == "individual_reward" else dict(rtol=1e-9, atol=1e-9)
+            np.testing.assert_allclose(info[:, _info_col(k)], z["info_num"][t][:, j], err_msg=ctx + " info " + k,
+                                       **tol)
+        np.testing.assert_allclose(env.state().cpu().numpy()[0], z["state"][t], rtol=0, atol=STATE_ATOL,
+                                   err_msg=ctx)
+        np.testing.assert_allclose(obs[0], z["obs"][t], rtol=0, atol=F32_ATOL, err_msg=ctx)
+        np.testing.assert_array_equal(adj_bits(adj[0]), z["adj_bits"][t], err_msg=ctx)
+        key = "t%03d_node" % t
+        if key in z.files:
+            np.testing.assert_allclose(node[0], z[key], rtol=0, atol=F32_ATOL, err_msg=ctx)
+            np.testing.assert_allclose(adj[0], z["t%03d_adj" % t], rtol=0, atol=F32_ATOL, err_msg=ctx)
+            e = np.stack(np.nonzero(env.t_edges.cpu().numpy()[0]))
+            np.testing.assert_array_equal(e, z["t%03d_edges" % t], err_msg=ctx)
+        if (t + 1) % meta["episode_length"] == 0 and t + 1 < steps:
+            obs, aid, node, adj, ep = env.reset(step_ep(z, meta, t))
+            assert z["resets_t"][n_reset] == t + 1
+            np.testing.assert_allclose([ep[0][k] for k in EPKEYS], z["resets_info"][n_reset], rtol=1e-9,
+                                       atol=1e-9, err_msg=ctx)
+            np.testing.assert_allclose(env.state().cpu().numpy()[0], z["t%03d_reset_state" % t], rtol=0,
+                                       atol=STATE_ATOL, err_msg=ctx)
+            np.testing.assert_allclose(obs[0], z["t%03d_reset_obs" % t], rtol=0, atol=F32_ATOL, err_msg=ctx)
+            np.testing.assert_allclose(node[0], z["t%03d_reset_node" % t], rtol=0, atol=F32_ATOL, err_msg=ctx)
+            np.testing.assert_allclose(adj[0], z["t%03d_reset_adj" % t], rtol=0, atol=F32_ATOL, err_msg=ctx)
+            n_reset += 1
+    env.close()
+
+
+@pytest.mark.parametrize("name", ["ba_merge_n8", "ba_cross_n4", "ev_di_lrmland_n4"])
+def test_gpu_layout_multi_env_matches_oracle(name):
+    """5 envs (seeds seed + 1000 k: their own layouts, timers and departures) with random actions
+    against the oracle over one episode and a second reset."""
+    from oracle.lsm_oracle import OracleEnv
+    z, meta = load(name)
+    lay, m = layout_for(meta)
+    n, seed = 5, 101
+    env = _gpu_layout_env(meta, n_envs=n, seed=seed)
+    vt, tt = tables_for(meta)
+    oras = [OracleEnv(m, seed + 1000 * k, table_dict(vt), table_dict(tt), integrator="restated")
+            for k in range(n)]
+    rngs = [np.random.RandomState(seed + 1000 * k) for k in range(n)]
+    ep = meta["ep"]
+    steps = min(meta["episode_length"], 160)
+    for rep in range(2):
+        g = env.reset(ep)
+        for k in range(n):
+            o = oras[k].reset(ep, lay.draw(rngs[k], oras[k].s))
+            np.testing.assert_allclose(g[0][k], np.array(o[0]), rtol=0, atol=F32_ATOL)
+        arng = np.random.default_rng(rep)
+        for t in range(steps):
+            a = arng.integers(0, 25, (n, meta["num_agents"]))
+            g = env.step(a, ep)
+            st = env.state().cpu().numpy()
+            dep = env.t_departed.cpu().numpy() if env.t_departed is not None else None
+            for k in range(n):
+                o = oras[k].step(a[k])
+                ctx = "%s env %d rep %d step %d" % (name, k, rep, t)
+                np.testing.assert_array_equal(g[5][k], np.array(o[5]), err_msg=ctx)
+                np.testing.assert_allclose(st[k], oras[k].s, rtol=0, atol=STATE_ATOL, err_msg=ctx)
+                np.testing.assert_allclose(g[4][k], np.array(o[4]), rtol=1e-6, atol=1e-5, err_msg=ctx)
+                np.testing.assert_allclose(g[0][k], np.array(o[0]), rtol=0, atol=F32_ATOL, err_msg=ctx)
+                np.testing.assert_array_equal(g[3][k] != 0, np.array(o[3]) != 0, err_msg=ctx)
+                if dep is not None:
+                    np.testing.assert_array_equal(dep[k], oras[k].departed, err_msg=ctx)
+    env.close()
+
+
+def test_gpu_layout_rejects_training_calls():
+    from lsm import capi
+    z, meta = load("ba_merge_n8")
+    env = _gpu_layout_env(meta)
+    import ctypes as C
+    from lsm.curriculum import curriculum_block, to_struct
+    cur = to_struct(curriculum_block(env.args, 4))
+    assert env.lib.lsm_reset(env.h, C.byref(cur), env._stream()) != 0   # layouts reset via lsm_reset_layout
+    assert "lsm_reset_layout" in env.lib.lsm_last_error(env.h).decode()
+    env.close()
+    with pytest.raises(ValueError):
+        from lsm.config import EnvArgs
+        from lsm.vec_env import GpuGraphVecEnv
+        args = EnvArgs.from_namespace(type("A", (), meta)())
+        vt, tt = tables_for(meta)
+        GpuGraphVecEnv(args, num_envs=1, device="cuda:0", value_table=vt, ttr_table=tt, auto_reset=True)
+    with pytest.raises(capi.LsmError):   # departures need airtaxi: refused at create
+        cfg = capi.LsmConfig(dynamics=0, num_envs=1, num_agents=4, num_landmarks=2, episode_length=10,
+                             world_size=4, scenario=capi.LSM_SCENARIO_DEPARTURES)
+        h = C.c_void_p()
+        lib = capi.load_library()
+        rc = lib.lsm_create(C.byref(cfg), C.byref(h))
+        try:
+            capi.check(rc, h)
+        finally:
+            lib.lsm_destroy(h)
+
+
+@pytest.mark.parametrize("dyn,n,kernel", [("double_integrator", 8, "team"), ("double_integrator", 8, "block"),
+                                          ("airtaxi", 16, "team"), ("double_integrator", 5, "wave")])
+def test_gpu_philox_reset(dyn, n, kernel, monkeypatch):
+    """LSM_RNG_PHILOX: reset 0 of env k equals lsm_host_scenario(Philox, key seed + 1000 k); across
+    auto-resets every scenario stays in the reference's boxes and differs from the previous one."""
+    import ctypes as C
+    from lsm import capi, curriculum
+    from lsm.config import EnvArgs
+    from lsm.vec_env import GpuGraphVecEnv
+    if kernel == "block":
+        monkeypatch.setenv("LSM_KERNEL", "block")
+    ws = 4 if dyn == "double_integrator" else 6
+    args = EnvArgs(dynamics_type=dyn, num_agents=n, world_size=ws, episode_length=12, num_env_steps=12 * 4,
+                   use_safety_filter=True, seed=9)
+    nenv = 64
+    env = GpuGraphVecEnv(args, num_envs=nenv, device="cuda:0", rng="philox", small_tables=True,
+                         return_numpy=False)
+    env.reset(4)
+    st0 = env.state().cpu().numpy().copy()
+    lib = capi.load_library()
+    cfg = capi.LsmConfig(dynamics=0 if dyn == "double_integrator" else 1, num_envs=1, num_agents=n,
+                         num_landmarks=2, episode_length=12, world_size=ws, rng=capi.LSM_RNG_PHILOX)
+    cur = curriculum.to_struct(curriculum.curriculum_block(args, 4))
+    for k in (0, 1, 17, nenv - 1):
+        st = np.zeros((n, 4))
+        lm = np.zeros((2 * n, 4))
+        lib.lsm_host_scenario(C.byref(cfg), C.byref(cur), 9 + 1000 * k, st.ctypes.data, lm.ctypes.data)
+        np.testing.assert_array_equal(st0[k], st)
+    rng = np.random.default_rng(0)
+    prev = st0
+    for t in range(30):
+        env.step(rng.integers(0, 25, (nenv, n)), 4)
+        if (t + 1) % 12 == 0:   # every env reset (episode end): a fresh scenario
+            cur_st = env.state().cpu().numpy()
+            assert bool(env.t_reset.all())
+            assert not np.array_equal(cur_st[:, :, :2], prev[:, :, :2])
+            if dyn == "double_integrator":
+                assert np.all(np.abs(cur_st[:, :, :2]) <= 0.8 * ws) and np.all(cur_st[:, :, 2:] == 0)
+            else:
+                assert np.all(cur_st[:, :, 0] <= 0.25 * ws) and np.all(np.abs(cur_st[:, :, 1]) <= 0.5 * ws)
+            prev = cur_st.copy()
+    assert np.isfinite(env.t_obs.cpu().numpy()).all()
+    env.close()
