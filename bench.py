@@ -241,6 +241,8 @@ def main():
     ap.add_argument("--edges", action="store_true",
                     help="also time GNNBase.process_adj (lsm_edges.hip) on the final adjacency and add an "
                          "'edges' object to the JSON line (SURVEY 8(f) row 2; not part of the step)")
+    ap.add_argument("--rng", default="mt19937", choices=("mt19937", "philox"),
+                    help="device reset stream: mt19937 = the reference's draws (default), philox = fast mode")
     ap.add_argument("--dry-run", action="store_true",
                     help="no GPU: check the rank launch, env offsets and collectives with gloo")
     a = ap.parse_args()
@@ -283,7 +285,8 @@ def main():
     from lsm.vec_env import GpuGraphVecEnv
     layout = c.get("adj_layout", "reference")
     env = GpuGraphVecEnv(args, num_envs=n_envs, device=dev, value_table=vt, ttr_table=tt,
-                         env_offset=rank * n_envs, return_numpy=False, build_infos=False, adj_layout=layout)
+                         env_offset=rank * n_envs, return_numpy=False, build_infos=False, adj_layout=layout,
+                         rng=a.rng)
     N = c["num_agents"]
     epl = c["episode_length"]
     pre = timed_window(a.warmup, a.steps, epl)
@@ -363,6 +366,7 @@ def main():
                                          "u64 disconnect masks, lossless)"),
                        "hj_table": "synthetic %s" % (str(vt.shape) if vt is not None else "none"),
                        "parallelism": "env-sharded dp%d" % world,
+                       "reset_rng": a.rng,
                        "handoff": ("DeviceGraphBuffer rows (ring-bound outputs + insert kernel)" if a.buffer
                                    else "env output tensors")},
             "ranks": {"rccl_world_size": (dist.get_world_size() if world > 1 else 1), "ms_per_step": per_rank},

@@ -219,9 +219,10 @@ struct Lds {
   double* scen;      // [SCEN_WS]
   double* scratch;   // [2][MAXN]
   // U2
-  double* dpair;     // [N][N]
-  float* vpair;      // [N][N]
-  uint8_t* inr;      // [N][N]
+  double* dpair;     // [N][N] [other j][ego i] (ego fastest)
+  double* vpair;     // [N][N] [other j][ego i] float32 values held as float64: the team kernel's
+                     // agent wave then reads 8-B words from G env blocks without bank conflicts
+  uint8_t* inr;      // [N][N] [other j][ego i]
   double* feat;      // [2N + NL][F] DI entity rows: agents pre, agents post, landmarks
   double* egooff;    // [N][F] DI ego offsets
   float* stage;      // [64][F] airtaxi node staging
@@ -390,7 +391,7 @@ __host__ __device__ inline LdsPlan lds_plan(int N, int NL, int E, int F, bool bl
   o = u1 + u1sz;
   // U2
   const size_t u2 = o;
-  size_t f1 = align16(8 * N * N), f2 = f1 + align16(4 * N * N), f3 = f2 + align16(N * N);
+  size_t f1 = align16(8 * N * N), f2 = f1 + align16(8 * N * N), f3 = f2 + align16(N * N);
   // DI entity rows + ego offsets; airtaxi: the [4][N] heading trig table (feat) only
   size_t g1 = F == 10 ? align16(8 * (2 * N + NL) * F) : align16(8 * 4 * N);
   size_t g2 = g1 + (F == 10 ? align16(8 * N * F) : 0);
@@ -440,7 +441,7 @@ __device__ __forceinline__ Lds carve(unsigned char* base, int N, int NL, int E, 
   L.scen = (double*)(base + p.off[k++]);
   L.scratch = (double*)(base + p.off[k++]);
   L.dpair = (double*)(base + p.off[k++]);
-  L.vpair = (float*)(base + p.off[k++]);
+  L.vpair = (double*)(base + p.off[k++]);
   L.inr = (uint8_t*)(base + p.off[k++]);
   L.feat = (double*)(base + p.off[k++]);
   L.egooff = (double*)(base + p.off[k++]);
@@ -989,15 +990,15 @@ __device__ __forceinline__ void filter_ego(const KParams& P, Lds& S, int i, uint
   float vmin = 0.0f;
   for (int j = 0; j < N; ++j) {
     if (j == i || inactive_pre(S, j)) continue;
-    const double d = S.dpair[i * N + j];
-    const float v = S.vpair[i * N + j];
+    const double d = S.dpair[j * N + i];   // pair matrices are [other][ego]: the lanes of an
+    const float v = (float)S.vpair[j * N + i];    // agent wave read consecutive words
     if (jd < 0 || d < dmin) { jd = j; dmin = d; }
     if (jv < 0 || v < vmin) { jv = j; vmin = v; }
   }
   if (jd < 0) return;  // no other active agent
   dec = jv;
   if (dmin > P.coord_range) return;
-  if (!S.inr[i * N + jv]) return;
+  if (!S.inr[jv * N + i]) return;
   filter_apply<DYN, NT>(P, S, i, jv, vmin, filtered, u0, u1);
 }
 
@@ -2180,7 +2181,7 @@ __device__ __forceinline__ void episode_stats(const KParams& P, Lds& S, int N, i
     double mn = INFINITY;
     for (int j = 0; j < N; ++j) {
       if (((m >> i) | (m >> j)) & 1ull) continue;
-      const double d = S.aa[i * N + j];
+      const double d = S.aa[j * N + i];   // symmetric; column reads are conflict-free
       if (!(d < P.coord_range && d > 0)) continue;
       cnt++;
       if (d < P.world_eng) neng++;
@@ -2197,7 +2198,7 @@ __device__ __forceinline__ void min_relative(Lds& S, int N, int i) {
   if (!inactive_pre(S, i)) {
     for (int j = 0; j < N; ++j) {
       if (j == i || inactive_pre(S, j)) continue;
-      const double d = S.aa2[i * N + j];
+      const double d = S.aa2[j * N + i];
       m = (d < m) ? d : m;
     }
   }
@@ -2208,7 +2209,7 @@ __device__ __forceinline__ void min_relative(Lds& S, int N, int i) {
 __device__ __forceinline__ int collision_count(const Lds& S, int N, int i) {
   int cc = 0;
   for (int a = 0; a < N; ++a)
-    if (a != i && S.aa2[i * N + a] < 1.05 * (0.05 + 0.05)) cc++;
+    if (a != i && S.aa2[a * N + i] < 1.05 * (0.05 + 0.05)) cc++;
   return cc;
 }
 
@@ -2369,7 +2370,7 @@ __global__ __launch_bounds__(64, DYN == 0 ? (LPE == 64 ? 4 : 2) : LSM_WAVES_PER_
     const SepChain sc = sep_chain(S.sep);
     const int npairs = N * N;
     for (int p = lane; p < npairs; p += LPE) {
-      const int i = p / N, j = p - i * N;
+      const int j = p / N, i = p - j * N;   // [j][i]: ego i fastest (bank-conflict-free reads)
       if (i == j || inactive_pre(S, i) || inactive_pre(S, j)) continue;
       const double ex = S.ps[i], ey = S.ps[N + i], ox = S.ps[j], oy = S.ps[N + j];
       S.dpair[p] = sqrt((ox - ex) * (ox - ex) + (oy - ey) * (oy - ey));

@@ -145,7 +145,7 @@ void rollout_team_kernel(const KParams* __restrict__ Pp, const KStep K) {
     if (filter_on) {
       const SepChain sc = sep_chain(S.sep);
       for (int p = lane; p < N * N; p += LPE) {
-        const int i = p / N, j = p - i * N;
+        const int j = p / N, i = p - j * N;   // [j][i]: ego i fastest (bank-conflict-free reads)
         if (i == j || S.dpre[i] || S.dpre[j]) continue;
         const double ex = S.ps[i], ey = S.ps[N + i], ox = S.ps[j], oy = S.ps[N + j];
         S.dpair[p] = sqrt((ox - ex) * (ox - ex) + (oy - ey) * (oy - ey));
