@@ -83,9 +83,36 @@ def build_variant(name: str, defines, verbose: bool = True) -> str:
     return out
 
 
+def build_variants(specs, verbose: bool = True):
+    """Several A/B variants at once: the product library and each variant's rollout object
+    compile in parallel (one hipcc process each), then each variant links. specs: NAME:D1,D2."""
+    import threading
+    t = threading.Thread(target=build, kwargs={"verbose": verbose})
+    t.start()
+    procs = []
+    for spec in specs:
+        name, _, defs = spec.partition(":")
+        obj = os.path.join(CSRC, "liblsm_rollout_%s.o" % name)
+        cmd = [HIPCC] + FLAGS + ["-D%s" % d for d in filter(None, defs.split(","))] + ["-c", "-o", obj, "lsm_rollout.hip"]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        procs.append((name, obj, subprocess.Popen(cmd, cwd=CSRC, stderr=subprocess.DEVNULL)))
+    t.join()
+    for name, obj, pr in procs:
+        if pr.wait() != 0:
+            raise RuntimeError("variant %s failed to compile" % name)
+        out = os.path.join(CSRC, "liblsm_rollout_%s.so" % name)
+        objs = [obj] + [_obj(u) for u in UNITS if u != "lsm_rollout.hip"]
+        subprocess.check_call([HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", out] + objs, cwd=CSRC)
+        os.remove(obj)
+
+
 if __name__ == "__main__":
     if len(sys.argv) > 2 and sys.argv[1] == "variant":
         # python -m lsm.build variant NAME DEF1 [DEF2 ...]
         build_variant(sys.argv[2], sys.argv[3:])
+    elif len(sys.argv) > 2 and sys.argv[1] == "variants":
+        # python -m lsm.build variants NAME:DEF1,DEF2 NAME2:DEF3 ...
+        build_variants(sys.argv[2:])
     else:
         build(force="--force" in sys.argv)
