@@ -141,6 +141,7 @@ struct OutDev {
 struct KParams {
   int n_envs, N, L, NL, E, F, OBS, dyn, episode_length, use_masking, use_filter_arg, auto_reset;
   int adj_compact;   // LSM_ADJ_COMPACT: unmasked E x E table once per env + per-ego masks
+  int lean;          // the team kernel carves the lean LDS layout (lds_plan)
   int filter_search; // workgroup kernel's HJ argmin: 1 bound-pruned (default), 0 every pair exact
   int scenario;      // LSM_SCENARIO_*
   int rng;           // LSM_RNG_*
@@ -180,6 +181,10 @@ struct KStep {
 // N = 8 so LDS does not cap residency below the VGPR limit (16 waves / CU):
 //   U1 = {fval, aa, aa2} (step)         | {mt, scen, scratch} (reset) | {stage} (node output, last)
 //   U2 = {dpair, vpair, inr} (filter)   | {feat, egooff} (DI node rows) | magnetic partial sums
+// The lean layout (airtaxi team kernel at N = 16: 19.3 instead of 25.5 KB per env, so 4
+// two-env workgroups fit a CU's 160 KB instead of 3) keeps the filter's pair matrices in U1
+// (dead before the distances are computed), leaves U2 to the info rows and the node tables,
+// and drops fval's landmark-landmark block (its values are the episode's lmd cache).
 // ----------------------------------------------------------------------------------
 __host__ __device__ inline size_t align16_(size_t x) { return (x + 15) & ~(size_t)15; }
 
@@ -212,7 +217,9 @@ struct Lds {
   uint64_t* emask;   // [N] bit r: entity r disconnected for ego e (snapshot rule)
   double* ecs;       // [2][N] cos / sin of the heading at step start (airtaxi filter frame)
   // U1
-  float* fval;       // [E][E] d if 0 < d < range else 0 (float32, unmasked)
+  float* fval;       // [E][E] d if 0 < d < range else 0 (float32, unmasked); lean: rows < N
+                     // [N][E], then the landmark rows' agent columns [NL][N] (fv4; the
+                     // landmark-landmark block is read from lmd)
   double* aa;        // [N][N] float64 agent-agent distances (episode stats)
   double* aa2;       // [N][N] np.linalg.norm agent-agent distances (min relative distance, collisions)
   uint32_t* mt;      // [MT_WORDS]
@@ -226,6 +233,8 @@ struct Lds {
   double* feat;      // [2N + NL][F] DI entity rows: agents pre, agents post, landmarks
   double* egooff;    // [N][F] DI ego offsets
   float* stage;      // [64][F] airtaxi node staging
+  double* info;      // [N][LSM_INFO_FIELDS] info rows staged for the coalesced copy-out (U2 base)
+  bool lean;         // the lean one-wave layout (lds_plan): see fval and the U1 / U2 note
   // workgroup-per-env kernel only (lsm_block.h)
   double* ex;        // [E] entity x (agents after integration, then landmarks)
   double* ey;        // [E]
@@ -336,7 +345,8 @@ __device__ __forceinline__ bool group_all(bool v) {
 // The record prefix (fields 0..14) is common to both kernels; the workgroup kernel keeps no
 // landmark-distance cache (lmd, 0 bytes), no E x E / N x N tables, and adds the entity
 // position table, per-ego multi-word masks and a node staging area.
-__host__ __device__ inline LdsPlan lds_plan(int N, int NL, int E, int F, bool block = false) {
+__host__ __device__ inline LdsPlan lds_plan(int N, int NL, int E, int F, bool block = false,
+                                            bool lean = false) {
   LdsPlan p;
   size_t o = 0;
   int k = 0;
@@ -381,23 +391,26 @@ __host__ __device__ inline LdsPlan lds_plan(int N, int NL, int E, int F, bool bl
   }
   // U1
   const size_t u1 = o;
-  size_t a = align16(4 * E * E), a2 = a + align16(8 * N * N), b = a2 + align16(8 * N * N);
+  const size_t fvb = lean ? (size_t)4 * (N * E + NL * N) : (size_t)4 * E * E;
+  size_t a = align16(fvb), a2 = a + align16(8 * N * N), b = a2 + align16(8 * N * N);
   size_t c = align16(4 * MT_WORDS), d = c + align16(8 * SCEN_WS), e = d + align16(8 * 2 * MAXN);
   p.off[k++] = u1; p.off[k++] = u1 + a; p.off[k++] = u1 + a2; p.off[k++] = u1; p.off[k++] = u1 + c;
   p.off[k++] = u1 + d;
   size_t u1sz = b > e ? b : e;
   const size_t h0 = align16(4 * WAVE * F);   // node staging for up to 64 pairs
   u1sz = u1sz > h0 ? u1sz : h0;
+  size_t f1 = align16(8 * N * N), f2 = f1 + align16(8 * N * N), f3 = f2 + align16(N * N);
+  if (lean) u1sz = u1sz > f3 ? u1sz : f3;   // the pair matrices at the head of U1
   o = u1 + u1sz;
   // U2
   const size_t u2 = o;
-  size_t f1 = align16(8 * N * N), f2 = f1 + align16(8 * N * N), f3 = f2 + align16(N * N);
+  const size_t pb = lean ? u1 : u2;   // pair matrices
   // DI entity rows + ego offsets; airtaxi: the [4][N] heading trig table (feat) only
   size_t g1 = F == 10 ? align16(8 * (2 * N + NL) * F) : align16(8 * 4 * N);
   size_t g2 = g1 + (F == 10 ? align16(8 * N * F) : 0);
-  p.off[k++] = u2; p.off[k++] = u2 + f1; p.off[k++] = u2 + f2;
+  p.off[k++] = pb; p.off[k++] = pb + f1; p.off[k++] = pb + f2;
   p.off[k++] = u2; p.off[k++] = u2 + g1; p.off[k++] = u1;   // stage aliases U1 (adj emitted first)
-  size_t m = f3 > g2 ? f3 : g2;
+  size_t m = lean ? g2 : (f3 > g2 ? f3 : g2);
   if (F == 10) m = m > (size_t)(8 * 2 * 64) ? m : (size_t)(8 * 2 * 64);   // magnetic partials (DI, filter off)
   m = m > (size_t)(8 * LSM_INFO_FIELDS * N) ? m : (size_t)(8 * LSM_INFO_FIELDS * N);   // info rows
   o = u2 + m;
@@ -405,8 +418,8 @@ __host__ __device__ inline LdsPlan lds_plan(int N, int NL, int E, int F, bool bl
   return p;
 }
 
-__device__ __forceinline__ Lds carve(unsigned char* base, int N, int NL, int E, int F) {
-  const LdsPlan p = lds_plan(N, NL, E, F);
+__device__ __forceinline__ Lds carve(unsigned char* base, int N, int NL, int E, int F, bool lean = false) {
+  const LdsPlan p = lds_plan(N, NL, E, F, false, lean);
   Lds L;
   int k = 0;
   L.ps = (double*)(base + p.off[k++]);
@@ -446,6 +459,8 @@ __device__ __forceinline__ Lds carve(unsigned char* base, int N, int NL, int E, 
   L.feat = (double*)(base + p.off[k++]);
   L.egooff = (double*)(base + p.off[k++]);
   L.stage = (float*)(base + p.off[k++]);
+  L.info = L.feat;   // U2 base (= dpair outside the lean layout)
+  L.lean = lean;
   L.ex = L.ey = nullptr;
   L.ccnt = nullptr;
   L.mpre = L.mpost = nullptr;
@@ -508,6 +523,8 @@ __device__ __forceinline__ Lds carve_block(unsigned char* base, int N, int NL, i
   L.dpair = (double*)(base + p.off[k++]);
   L.stage = (float*)(base + p.off[k++]);
   L.fval = nullptr; L.aa = nullptr; L.aa2 = nullptr; L.vpair = nullptr; L.inr = nullptr;
+  L.info = L.dpair;
+  L.lean = false;
   L.dep0 = L.dep1 = L.tmr = nullptr;
   L.ith = L.pth = L.psp = L.trig1 = nullptr;
   return L;
@@ -1292,6 +1309,32 @@ __device__ __forceinline__ void build_rows_di(const KParams& P, Lds& S) {
   }
 }
 
+// The thresholded distance table fval: entries (r, c) and float4 groups (c % 4 == 0) of either
+// layout. Lean layout (N % 4 == 0, E % 4 == 0): agent rows [N][E], landmark rows' agent columns
+// [NL][N], the landmark-landmark block from the episode cache lmd (diagonal 0).
+__device__ __forceinline__ float fv_ll(const Lds& S, int NL, int la, int lb) {
+  if (la == lb) return 0.0f;
+  const int lo = la < lb ? la : lb, hi = la < lb ? lb : la;
+  return S.lmd[lo * (2 * NL - lo - 1) / 2 + (hi - lo - 1)];
+}
+__device__ __forceinline__ float4 fv4(const Lds& S, int N, int NL, int E, int r, int c) {
+  if (!S.lean || r < N) return *(const float4*)(S.fval + r * E + c);
+  if (c < N) return *(const float4*)(S.fval + N * E + (r - N) * N + c);
+  const int la = r - N, lb = c - N;
+  return make_float4(fv_ll(S, NL, la, lb), fv_ll(S, NL, la, lb + 1), fv_ll(S, NL, la, lb + 2),
+                     fv_ll(S, NL, la, lb + 3));
+}
+__device__ __forceinline__ float fv1(const Lds& S, int N, int NL, int E, int r, int c) {
+  if (!S.lean || r < N) return S.fval[r * E + c];
+  if (c < N) return S.fval[N * E + (r - N) * N + c];
+  return fv_ll(S, NL, r - N, c - N);
+}
+// store entry (r, c); the lean layout keeps no landmark-landmark entries
+__device__ __forceinline__ void fv_set(Lds& S, int N, int E, int r, int c, float v) {
+  if (!S.lean || r < N) S.fval[r * E + c] = v;
+  else if (c < N) S.fval[N * E + (r - N) * N + c] = v;
+}
+
 // node_obs [N][E][F] and adj [N][E][E] of one env. Node rows are computed per (ego, entity)
 // pair by one lane, staged in LDS, and copied out as contiguous float4 when the env block is
 // 16-byte aligned; the adjacency is a masked select over the thresholded distance table,
@@ -1317,7 +1360,7 @@ __device__ __forceinline__ void emit_adj_uniform(const KParams& P, const Lds& S,
       u[j] = 4 * (t < last ? t : last);
       const int r = qdiv<NT>(u[j], E, P.m_E);
       const int c = u[j] - r * E;
-      w[j] = *(const float4*)(S.fval + u[j]);
+      w[j] = fv4(S, N, NL, E, r, c);
       const uint32_t bits = ((m >> r) & 1ull) ? 0xfu : ((uint32_t)(m >> c) & 0xfu);
       if (bits & 1u) w[j].x = 0.f;
       if (bits & 2u) w[j].y = 0.f;
@@ -1359,9 +1402,15 @@ __device__ __forceinline__ void emit_graph(const KParams& P, Lds& S, int env, bo
     // LSM_ADJ_COMPACT: the unmasked table once + the per-ego masks (one word: E <= 64)
     GAS float* a = gptr(P.o.adj) + (size_t)env * EE;
     if ((E & 3) == 0) {
-      for (int q = lane; q < EE / 4; q += LPE) st_stream<(NT >= 16)>(a + 4 * q, *(const float4*)(S.fval + 4 * q));
+      for (int q = lane; q < EE / 4; q += LPE) {
+        const int r = qdiv<NT>(4 * q, E, P.m_E);
+        st_stream<(NT >= 16)>(a + 4 * q, fv4(S, N, NL, E, r, 4 * q - r * E));
+      }
     } else {
-      for (int q = lane; q < EE; q += LPE) a[q] = S.fval[q];
+      for (int q = lane; q < EE; q += LPE) {
+        const int r = qdiv<NT>(q, E, P.m_E);
+        a[q] = fv1(S, N, NL, E, r, q - r * E);
+      }
     }
     if (lane < N) gptr(P.o.adjmask)[(size_t)env * N + lane] = S.emask[lane];
   } else if ((E & 3) == 0 && uni) {
@@ -1379,7 +1428,7 @@ __device__ __forceinline__ void emit_graph(const KParams& P, Lds& S, int env, bo
         const int t = t0 + j * LPE;
         u[j] = 4 * (t < last ? t : last);
         rr[j] = qdiv<NT>(u[j], E, P.m_E);
-        v[j] = *(const float4*)(S.fval + u[j]);
+        v[j] = fv4(S, N, NL, E, rr[j], u[j] - rr[j] * E);
       }
       for (int e = 0; e < N; ++e) {
         const uint64_t m = S.emask[e];
@@ -1405,7 +1454,7 @@ __device__ __forceinline__ void emit_graph(const KParams& P, Lds& S, int env, bo
       const int r = qdiv<NT>(u, E, P.m_E);
       const int c = u - r * E;
       const uint64_t m = S.emask[e];
-      adj_out[q] = (((m >> r) | (m >> c)) & 1ull) ? 0.0f : S.fval[u];
+      adj_out[q] = (((m >> r) | (m >> c)) & 1ull) ? 0.0f : fv1(S, N, NL, E, r, c);
     }
   }
   emit_nodes<DYN, LPE, NT>(P, S, env, uni);
@@ -1535,8 +1584,8 @@ __device__ __forceinline__ void compute_dist(const KParams& P, Lds& S, const uin
     const double dx = xa - xb, dy = ya - yb;
     const double d = sqrt(dx * dx + dy * dy);   // |p_a - p_b| == |p_b - p_a| bit for bit
     const float fv = (d < P.coord_range && d > 0) ? (float)d : 0.0f;
-    S.fval[a * E + b] = fv;
-    S.fval[b * E + a] = fv;
+    fv_set(S, N, E, a, b, fv);
+    fv_set(S, N, E, b, a, fv);
     if (t >= nmov) S.lmd[t - nmov] = fv;
     if (b < N) {
       const double d2 = blas_norm2(dx, dy);
@@ -1546,7 +1595,7 @@ __device__ __forceinline__ void compute_dist(const KParams& P, Lds& S, const uin
       S.aa2[b * N + a] = d2;
     }
   }
-  if (!full) {
+  if (!full && !S.lean) {
     // landmark block from the episode cache: u = (la, lb) over NL x NL (diagonal -> 0 below)
     for (int u = lane; u < NL * NL; u += LPE) {
       const int la = qdiv<NT>(u, NL, P.m_NL), lb = u - la * NL;
@@ -1556,7 +1605,7 @@ __device__ __forceinline__ void compute_dist(const KParams& P, Lds& S, const uin
     }
   }
   for (int k = lane; k < E; k += LPE) {
-    S.fval[k * E + k] = 0.0f;
+    fv_set(S, N, E, k, k, 0.0f);
     if (k < N) { S.aa[k * N + k] = 0.0; S.aa2[k * N + k] = 0.0; }
   }
   esync<LPE>();
@@ -2437,9 +2486,9 @@ __global__ __launch_bounds__(64, DYN == 0 ? (LPE == 64 ? 4 : 2) : LSM_WAVES_PER_
   // ---- 7/8. info_callback numbers -----------------------------------------------------
   if (lane < N) info_agent<DYN, NT>(P, S, lane, cstep, at, collision_count(S, N, lane));
   __syncthreads();
-  if (lane < N) info_row<NT>(P, S, lane, rew, S.dpair + lane * LSM_INFO_FIELDS);   // staged in U2
+  if (lane < N) info_row<NT>(P, S, lane, rew, S.info + lane * LSM_INFO_FIELDS);   // staged in U2
   __syncthreads();
-  rec_copy<LPE>((const f32x4*)S.dpair, (GAS f32x4*)(gptr(P.o.info) + (size_t)env * N * LSM_INFO_FIELDS),
+  rec_copy<LPE>((const f32x4*)S.info, (GAS f32x4*)(gptr(P.o.info) + (size_t)env * N * LSM_INFO_FIELDS),
                 N * LSM_INFO_FIELDS / 2);
   if (chunked) emit_adj_uniform<LPE, NT>(P, S, env, m_pre, N / 2, 3 * N / 4);
   STAMP(8);
@@ -2540,6 +2589,7 @@ struct lsm_env {
   bool block;   // workgroup-per-env kernel (N > 32 or E > 64, or LSM_KERNEL=block)
   bool generic_only;   // LSM_GENERIC=1: never use the compile-time-N kernels (tests): 64 (one env per wave), 32 or 16 (2 or 4 envs per wave)
   int team;   // envs per workgroup of the team kernel (lsm_team.h); 0 = rollout_kernel
+  bool lean;  // the team kernel's lean LDS layout (airtaxi, N % 4 == 0, E % 4 == 0)
 };
 
 static int fail(lsm_env* e, const std::string& msg) {
@@ -2581,6 +2631,7 @@ static void fill_params(const lsm_env* e, KParams& P) {
   P.seed = e->cfg.seed;
   P.env_offset = e->cfg.env_offset;
   P.lds_dep_off = (uint32_t)lds_plan(e->N, e->NL, e->E, e->F, e->block).bytes;
+  P.lean = e->lean ? 1 : 0;
   P.world_size = e->cfg.world_size;
   const double pi = 3.141592653589793;
   P.pi = pi;
@@ -2763,6 +2814,10 @@ int lsm_create(const lsm_config* cfg, lsm_env** out) {
       else if (e->team) return fail(e, "LSM_TEAM must be 0, 2, 4 or 8 with LSM_TEAM * num_agents <= 64");
     }
   }
+  // lean LDS layout for the airtaxi team kernel (3 -> 4 two-env workgroups per CU at N = 16);
+  // LSM_LEAN=0 keeps the full table (A/B)
+  e->lean = e->team && cfg->dynamics == LSM_AIRTAXI && (N & 3) == 0 && (e->E & 3) == 0;
+  if (const char* v = getenv("LSM_LEAN")) e->lean = e->lean && atoi(v) != 0;
   if (!(e->lpe == 16 || e->lpe == 32 || e->lpe == 64) || e->lpe < (e->block ? 1 : N))
     return fail(e, "LSM_LPE must be 16, 32 or 64 and >= num_agents");
   HIPCHK(e, hipGetDevice(&e->device));
@@ -3099,7 +3154,7 @@ static int launch_block_t(lsm_env* e, const KStep& L, size_t env_lds, hipStream_
 }
 
 static int launch(lsm_env* e, KStep& L, hipStream_t st) {
-  size_t env_lds = lds_plan(e->N, e->NL, e->E, e->F, e->block).bytes;
+  size_t env_lds = lds_plan(e->N, e->NL, e->E, e->F, e->block, e->lean).bytes;
   if (e->team) env_lds = team_env_bytes(env_lds, e->N);
   if (e->cfg.scenario == LSM_SCENARIO_DEPARTURES) env_lds += dep_lds_bytes(e->N);
   if (e->block ? env_lds > 160 * 1024

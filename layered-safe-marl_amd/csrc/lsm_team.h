@@ -68,14 +68,14 @@ void rollout_team_kernel(const KParams* __restrict__ Pp, const KStep K) {
   LSM_DIMS;
   const uint32_t B = P.lds_env_bytes;
   unsigned char* lbase = smem + (size_t)w * B;
-  Lds S = carve(lbase, N, NL, E, F);
+  Lds S = carve(lbase, N, NL, E, F, DYN == 1 && P.lean != 0);   // folds away for the DI kernels
   // agent view: lane = g * NT + i
   const int ag = lane / NT;
   const int ai = lane - ag * NT;
   const bool alane = ag < G && env0 + ag < P.n_envs;
   const int aslot = ag < G ? ag : 0;
   const int aenv = env0 + aslot;
-  Lds A = carve(smem + (size_t)aslot * B, N, NL, E, F);
+  Lds A = carve(smem + (size_t)aslot * B, N, NL, E, F, DYN == 1 && P.lean != 0);
   constexpr int WB = 0, WD = 1 % G;           // agent-phase waves (different SIMDs)
   TRTSTAMP(13);
   TSTAMP(0);
@@ -217,7 +217,7 @@ void rollout_team_kernel(const KParams* __restrict__ Pp, const KStep K) {
     esync<LPE>();
     TSTAMP(11);
     if (alane) {
-      info_row<NT>(P, A, ai, at.rew, A.dpair + ai * LSM_INFO_FIELDS);   // staged in U2
+      info_row<NT>(P, A, ai, at.rew, A.info + ai * LSM_INFO_FIELDS);   // staged in U2
       episode_stats<DYN>(P, A, N, ai);
     }
   } else if (live && chunked) {
@@ -229,7 +229,7 @@ void rollout_team_kernel(const KParams* __restrict__ Pp, const KStep K) {
 
   // ---- E. info rows, dones, then the auto-reset or what the speculation did not cover ----------
   if (!live) return;
-  rec_copy<LPE>((const f32x4*)S.dpair, (GAS f32x4*)(gptr(P.o.info) + (size_t)env * N * LSM_INFO_FIELDS),
+  rec_copy<LPE>((const f32x4*)S.info, (GAS f32x4*)(gptr(P.o.info) + (size_t)env * N * LSM_INFO_FIELDS),
                 N * LSM_INFO_FIELDS / 2);
   bool my_done = true;
   if (lane < N) {
