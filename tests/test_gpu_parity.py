@@ -137,8 +137,9 @@ def test_gpu_matches_oracle_multi_env(case, lpe, monkeypatch):
     team_spec = (c0["num_agents"], c0["dynamics_type"]) in ((8, "double_integrator"), (16, "airtaxi"))
     if lpe in ("t2", "t4", "t8", "64w") and not team_spec:
         pytest.skip("the team kernel is specialised for N = 8 double integrator and N = 16 airtaxi")
-    if lpe in ("t4", "t8") and c0["num_agents"] == 16:
-        pytest.skip("4 (8) airtaxi envs of 16 agents per workgroup: 98 KB of LDS (over 64 lanes)")
+    if lpe == "t8" and c0["num_agents"] == 16:
+        pytest.skip("8 airtaxi envs of 16 agents do not fit one 64-lane agent wave")
+    # "t4" at airtaxi N = 16: 4 envs x 19.3 KB in the lean LDS layout (77 KB per workgroup)
     partial = lpe in (16, 32, "t2", "t4", "t8")
     if lpe in ("t2", "t4", "t8", "64w"):
         monkeypatch.setenv("LSM_TEAM", "0" if lpe == "64w" else lpe[1:])
