@@ -181,8 +181,8 @@ struct KStep {
 // N = 8 so LDS does not cap residency below the VGPR limit (16 waves / CU):
 //   U1 = {fval, aa, aa2} (step)         | {mt, scen, scratch} (reset) | {stage} (node output, last)
 //   U2 = {dpair, vpair, inr} (filter)   | {feat, egooff} (DI node rows) | magnetic partial sums
-// The lean layout (airtaxi team kernel at N = 16: 19.3 instead of 25.5 KB per env, so 4
-// two-env workgroups fit a CU's 160 KB instead of 3) keeps the filter's pair matrices in U1
+// The lean layout (airtaxi team kernel at N = 16: 19.3 instead of 25.5 KB per env, so a CU's
+// 160 KB holds 8 envs instead of 6, its VGPR limit) keeps the filter's pair matrices in U1
 // (dead before the distances are computed), leaves U2 to the info rows and the node tables,
 // and drops fval's landmark-landmark block (its values are the episode's lmd cache).
 // ----------------------------------------------------------------------------------
@@ -2806,7 +2806,7 @@ int lsm_create(const lsm_config* cfg, lsm_env** out) {
   e->team = 0;
   if (!e->block && e->lpe == 64 && L == 2 && !e->generic_only) {
     if (cfg->dynamics == LSM_DOUBLE_INTEGRATOR && N == 8) e->team = 4;   // measured: 4 < 8 < 2 (us/step)
-    if (cfg->dynamics == LSM_AIRTAXI && N == 16) e->team = 2;
+    if (cfg->dynamics == LSM_AIRTAXI && N == 16) e->team = 4;   // lean LDS: 4 < 2 < 0 (us/step)
     if (const char* v = getenv("LSM_TEAM")) {
       const int g = atoi(v);
       if (g == 0) e->team = 0;
@@ -2814,7 +2814,7 @@ int lsm_create(const lsm_config* cfg, lsm_env** out) {
       else if (e->team) return fail(e, "LSM_TEAM must be 0, 2, 4 or 8 with LSM_TEAM * num_agents <= 64");
     }
   }
-  // lean LDS layout for the airtaxi team kernel (3 -> 4 two-env workgroups per CU at N = 16);
+  // lean LDS layout for the airtaxi team kernel (6 -> 8 envs per CU at N = 16);
   // LSM_LEAN=0 keeps the full table (A/B)
   e->lean = e->team && cfg->dynamics == LSM_AIRTAXI && (N & 3) == 0 && (e->E & 3) == 0;
   if (const char* v = getenv("LSM_LEAN")) e->lean = e->lean && atoi(v) != 0;

@@ -126,7 +126,7 @@ def test_gpu_matches_oracle_multi_env(case, lpe, monkeypatch):
     """16 (or 15: a partly filled last wave / workgroup) envs with per-env seeds seed + 1000 k,
     random actions, across an auto-reset; every kernel variant: 1, 2 or 4 envs/wave; at one env
     per wave the default dispatch ("64": the team kernel for N = 8 double integrator (8 envs per
-    workgroup) and N = 16 airtaxi (2 per workgroup), the compile-time-N rollout_kernel for
+    workgroup) and N = 16 airtaxi (4 per workgroup), the compile-time-N rollout_kernel for
     N = 3), the one-wave rollout_kernel forced ("64w", LSM_TEAM=0), the team kernel with 2 / 4
     envs per workgroup ("t2", "t4", "t8"; one fewer env than a whole number of workgroups), the
     generic kernel ("64g"), and the workgroup-per-env
