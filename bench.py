@@ -245,9 +245,12 @@ def main():
                     help="device reset stream: mt19937 = the reference's draws (default), philox = fast mode")
     ap.add_argument("--dry-run", action="store_true",
                     help="no GPU: check the rank launch, env offsets and collectives with gloo")
+    ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
+                    help="test only: gloo lets --gpus N ranks share one GPU (real device envs, CPU "
+                         "collectives); the product path and every reported number use nccl (RCCL)")
     a = ap.parse_args()
 
-    from lsm.dist import rank_info, global_episode_summary
+    from lsm.dist import rank_info, EpisodeSummaryReducer
     launched = "WORLD_SIZE" in os.environ
     if not launched and a.gpus > 1:
         sys.exit(launch(a))
@@ -277,10 +280,12 @@ def main():
     import torch.distributed as dist
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        dist.init_process_group("nccl")
+        dist.init_process_group(a.dist_backend)
         if dist.get_world_size() != a.gpus:
-            raise SystemExit("RCCL world size %d != --gpus %d" % (dist.get_world_size(), a.gpus))
-    dev = torch.device("cuda:%d" % local_rank)
+            raise SystemExit("%s world size %d != --gpus %d" % (a.dist_backend, dist.get_world_size(), a.gpus))
+    # one GPU per rank; the test-only gloo mode may put several ranks on one device
+    dev = torch.device("cuda:%d" % (local_rank % torch.cuda.device_count() if a.dist_backend == "gloo"
+                                    else local_rank))
     torch.cuda.set_device(dev)
     from lsm.vec_env import GpuGraphVecEnv
     layout = c.get("adj_layout", "reference")
@@ -290,11 +295,17 @@ def main():
     N = c["num_agents"]
     epl = c["episode_length"]
     pre = timed_window(a.warmup, a.steps, epl)
-    gen = torch.Generator(device=dev).manual_seed(1234 + rank)
     # Synthetic policy: every step's discrete actions drawn up front, resident in HBM before the
     # timed region (the policy is outside the path; one env-step = one rollout_kernel launch).
-    acts_all = torch.randint(0, 25, (pre + a.steps, n_envs, N), generator=gen, device=dev,
-                             dtype=torch.int32)
+    # Step t's actions for ALL global envs come from one generator seeded 1234 + t and each rank
+    # keeps its slice, so a sharded run steps exactly the envs of a single-process run.
+    gen = torch.Generator(device=dev)
+    acts_all = torch.empty((pre + a.steps, n_envs, N), dtype=torch.int32, device=dev)
+    for t in range(pre + a.steps):
+        gen.manual_seed(1234 + t)
+        full = torch.randint(0, 25, (world * n_envs, N), generator=gen, device=dev, dtype=torch.int32)
+        acts_all[t].copy_(full[rank * n_envs:(rank + 1) * n_envs])
+    del full
     buf = None
     if a.buffer:
         from lsm.buffer import DeviceGraphBuffer
@@ -302,6 +313,10 @@ def main():
         buf.warmup(ep)
     else:
         env.reset(ep)
+
+    # Episode boundary: the summary reduction and its RCCL collectives are enqueued without a
+    # host sync (lsm.dist.EpisodeSummaryReducer); the values are read after the timed region.
+    summaries = EpisodeSummaryReducer(n_envs, dev)
 
     def one_step(t):
         if buf is not None:
@@ -312,11 +327,13 @@ def main():
             env.step_async(acts_all[t], ep)
             env.step_wait()
         if (t + 1) % epl == 0:   # episode boundary: RCCL reduction of the episode summary
-            global_episode_summary(env.t_epinfo)
+            summaries.submit(env.t_epinfo)
 
-    global_episode_summary(env.t_epinfo)   # load the reduction kernels before any timed call
+    summaries.submit(env.t_epinfo)   # load the reduction kernels / RCCL before any timed call
+    summaries.results()
     for t in range(pre):
         one_step(t)
+    summaries.results()
     # Kernel time: HIP events on the launch stream bracketing the whole timed region (per-launch
     # event pairs would add their own GPU-side markers between back-to-back launches).
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -343,6 +360,13 @@ def main():
         per_rank = [float(x[0]) * 1e3 / a.steps for x in allt]
         elapsed = max(float(x[0]) for x in allt)
         kern_ms = max(float(x[1]) for x in allt)
+    ep_summaries = summaries.results()   # after the timed region: the boundary's global summary
+    offsets = [rank * n_envs]
+    if world > 1:
+        o = torch.tensor([env.env_offset], dtype=torch.float64, device=dev)
+        allo = [torch.zeros_like(o) for _ in range(world)]
+        dist.all_gather(allo, o)
+        offsets = [int(x.item()) for x in allo]
     total_agent_steps = world * n_envs * N * a.steps
     value = total_agent_steps / elapsed
     from lsm.perf_model import step_bytes
@@ -369,7 +393,8 @@ def main():
                        "reset_rng": a.rng,
                        "handoff": ("DeviceGraphBuffer rows (ring-bound outputs + insert kernel)" if a.buffer
                                    else "env output tensors")},
-            "ranks": {"rccl_world_size": (dist.get_world_size() if world > 1 else 1), "ms_per_step": per_rank},
+            "ranks": {"rccl_world_size": (dist.get_world_size() if world > 1 else 1), "ms_per_step": per_rank,
+                      "env_offsets": offsets, "backend": a.dist_backend if world > 1 else None},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
                          "frac": achieved / PEAK_HBM_GBPS, "traffic": traffic, "traffic_unit": "HBM bytes/launch (rocprofv3 PMC)",
                          "kernel": env.kernel_name,
@@ -377,6 +402,7 @@ def main():
                          "gather_bytes_per_launch": sb["gather_bytes"] * n_envs,
                          "bytes_model": "lsm/perf_model.py: record + outputs + HJ gathers (SURVEY 8(d))"},
             "cpu_baseline": cpu,
+            "episode_summaries_timed": ep_summaries,
         }
         if a.edges:
             line["edges"] = bench_edges(env, dev)

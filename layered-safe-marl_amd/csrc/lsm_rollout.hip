@@ -659,6 +659,9 @@ __device__ __forceinline__ bool interp_value(const TableDev& T, const double* s,
   int cell;
   float w[1 << ND];
   if (!grid_cell<ND>(T, s, cell, w)) return false;
+#ifdef LSM_XP_VALHOT   // diagnostic bound only (wrong values): every lookup in a 256 KB hot region
+  cell &= 4095;
+#endif
   const GAS f32x4* c4 = (const GAS f32x4*)(gptr(T.cells) + (size_t)cell * (1 << ND));
   float v[1 << ND];
 #pragma unroll
@@ -686,6 +689,9 @@ __device__ __forceinline__ void interp_grad(const TableDev& T, const double* s, 
     for (int d = 0; d < ND; ++d) g[d] = __builtin_nanf("");
     return;
   }
+#ifdef LSM_XP_GRADHOT   // diagnostic bound only (wrong values)
+  cell &= 4095;
+#endif
   const GAS f32x4* gc = (const GAS f32x4*)gptr(T.gcells) + (size_t)cell * (1 << ND) * T.gw;
 #pragma unroll
   for (int c = 0; c < (1 << ND); ++c) {
@@ -1937,9 +1943,14 @@ __device__ __forceinline__ void integrate_agent(const KParams& P, Lds& S, int N,
   double x = S.ps[i], y = S.ps[N + i], s2 = S.ps[2 * N + i], s3 = S.ps[3 * N + i];
   double spd;
   if (DYN == 0) {
+#ifdef LSM_XP_NORK   // diagnostic bound only: closed form instead of the RK45 restatement
+    x = x + s2 * dt + 0.5 * a0 * dt * dt; y = y + s3 * dt + 0.5 * a1 * dt * dt;
+    s2 = s2 + a0 * dt; s3 = s3 + a1 * dt;
+#else
     double yv[4] = {x, y, s2, s3};
     rk45_di(yv, a0, a1, dt);
     x = yv[0]; y = yv[1]; s2 = yv[2]; s3 = yv[3];
+#endif
     spd = sqrt(s2 * s2 + s3 * s3);
     if (spd > P.max_speed) {
       s2 = P.max_speed * s2 / spd;
@@ -2297,6 +2308,9 @@ __device__ __forceinline__ void decode_action(const KParams& P, Lds& S, int N, i
 template <int DYN, int NT>
 __device__ __forceinline__ void filter_agent(const KParams& P, Lds& S, int N, int i, bool filter_on) {
   double u0 = S.raw[i], u1 = S.raw[N + i];
+#ifdef LSM_XP_NOFILT   // diagnostic bound only: no filter
+  filter_on = false;
+#endif
   if (filter_on) {
     uint8_t fl = 0;
     int dec = -1;

@@ -221,7 +221,9 @@ void rollout_team_kernel(const KParams* __restrict__ Pp, const KStep K) {
       episode_stats<DYN>(P, A, N, ai);
     }
   } else if (live && chunked) {
+#ifndef LSM_XP_NOOUT   // diagnostic bound only: no graph outputs
     emit_adj_uniform<LPE, NT>(P, S, env, m_pre, 0, N);
+#endif
   }
   TSTAMP(8);
   __syncthreads();
@@ -248,7 +250,9 @@ void rollout_team_kernel(const KParams* __restrict__ Pp, const KStep K) {
   } else {
     if (lane == 0) gptr(P.o.reset_flag)[env] = 0;
     // adjacency already stored in D except WD's (emit_graph rewrites it if a status changed)
+#ifndef LSM_XP_NOOUT
     emit_graph<DYN, LPE, NT>(P, S, env, chunked && w != WD);
+#endif
     esync<LPE>();
     store_state<DYN, LPE, NT>(P, S, lbase, env, false);
   }

@@ -35,16 +35,56 @@ def shard(n_global: int, rank: int, world: int):
 
 
 def global_episode_summary(ep_info: torch.Tensor, group=None) -> dict:
-    """All-rank episode summary from each rank's [n_local, 8] float64 ep_info tensor."""
+    """All-rank episode summary from each rank's [n_local, 8] float64 ep_info tensor
+    (synchronous: returns host floats, like the runner's parse after a rollout)."""
+    r = EpisodeSummaryReducer(ep_info.shape[0], ep_info.device, group=group)
+    r.submit(ep_info)
+    return r.results()[0]
+
+
+def _dist_on():
     import torch.distributed as dist
-    s = ep_info.sum(dim=0)
-    cnt = torch.tensor([float(ep_info.shape[0])], dtype=ep_info.dtype, device=ep_info.device)
-    buf = torch.cat([s, cnt])
-    mn = ep_info[:, 6].min().reshape(1).clone()
-    if dist.is_available() and dist.is_initialized():
-        dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=group)
-        dist.all_reduce(mn, op=dist.ReduceOp.MIN, group=group)
-    mean = (buf[:8] / buf[8]).tolist()
-    out = dict(zip(EPKEYS, mean))
-    out["min_distance_min"] = float(mn.item())
-    return out
+    return dist.is_available() and dist.is_initialized()
+
+
+class EpisodeSummaryReducer:
+    """The per-episode-boundary reduction without a host synchronisation.
+
+    ``submit(ep_info)`` enqueues, on the current stream, the column sums and the
+    ``min_distance_min`` minimum of this rank's [n_local, 8] ep_info into fresh device
+    buffers and, when a process group is up, the two collectives as async work (RCCL runs
+    them stream-ordered after the sums; nothing waits on the host). ``results()`` waits
+    for everything submitted and returns one dict per boundary. The reference runner
+    likewise parses episode info once per episode, after the rollout
+    (graph_mpe_runner.py:155-162), not inside the step loop."""
+
+    def __init__(self, n_local: int, device, group=None):
+        self.group = group
+        self.device = torch.device(device)
+        # the env count rides in the SUM buffer (one collective gives sums and the global count)
+        self._cnt = torch.full((1,), float(n_local), dtype=torch.float64, device=self.device)
+        self._pending = []
+
+    def submit(self, ep_info: torch.Tensor):
+        buf = torch.empty(9, dtype=torch.float64, device=ep_info.device)
+        torch.sum(ep_info, dim=0, out=buf[:8])
+        buf[8:].copy_(self._cnt)
+        mn = torch.amin(ep_info[:, 6:7], dim=0)
+        works = ()
+        if _dist_on():
+            import torch.distributed as dist
+            works = (dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True),
+                     dist.all_reduce(mn, op=dist.ReduceOp.MIN, group=self.group, async_op=True))
+        self._pending.append((buf, mn, works))
+
+    def results(self):
+        out = []
+        for buf, mn, works in self._pending:
+            for w in works:
+                w.wait()
+            mean = (buf[:8] / buf[8]).tolist()
+            d = dict(zip(EPKEYS, mean))
+            d["min_distance_min"] = float(mn.item())
+            out.append(d)
+        self._pending = []
+        return out

@@ -125,6 +125,7 @@ class GpuGraphVecEnv(ShareVecEnv):
         if rng not in ("mt19937", "philox"):
             raise ValueError("rng must be 'mt19937' or 'philox'")
         self.num_envs = int(num_envs if num_envs is not None else a.n_rollout_threads)
+        self.env_offset = int(env_offset)   # global index of this handle's env 0 (seed + 1000 k)
         self.device = torch.device(device if device is not None else "cuda:%d" % torch.cuda.current_device())
         if self.device.type != "cuda":
             raise capi.LsmError("GpuGraphVecEnv needs a HIP device; there is no CPU fallback")
