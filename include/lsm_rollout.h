@@ -136,7 +136,9 @@ typedef struct lsm_config {
                                 (core.py:741-836), so it never changes the dynamics. Default 0. */
   int32_t scenario;          /* LSM_SCENARIO_TRAIN (default) / _LAYOUT / _DEPARTURES            */
   int32_t rng;               /* LSM_RNG_MT19937 (default) / LSM_RNG_PHILOX                      */
-  int32_t reserved1;
+  int32_t num_internal_step; /* args.num_internal_step (0 or 1 = one): World.step repeats filter ->
+                                action_diff -> integrate this many times per env step, then the
+                                distances and minimum relative distance (core.py:607-631)         */
 } lsm_config;
 
 /* Curriculum block for one reset call (navigation_graph_safe.py:324-366), computed by the
@@ -190,7 +192,10 @@ int lsm_step(lsm_env* env, const void* actions_device, int32_t action_kind,
  * which draws from the env's numpy stream on the host. `layout` is a DEVICE pointer to float64
  * [n][lsm_layout_doubles(env)]: agent state [N][4] (x, y, v_x|theta, v_y|speed), landmarks
  * [N*L][4] (x, y, heading, speed; landmark k = order * N + agent), and with
- * LSM_SCENARIO_DEPARTURES departed [N] (0/1), departure_timer [N], init_theta [N]. Everything
+ * LSM_SCENARIO_DEPARTURES departed [N] (0/1), departure_timer [N], init_theta [N]; last, one
+ * keep-done word: 0 = the layout sets every agent.done = False (all layouts but one), nonzero =
+ * agents done at the end of the previous episode stay done, unintegrated, with the layout's state
+ * as their frozen state (scenario_circular_config, navigation_graph_safe_eval.py:100-121). Everything
  * else of the reset (episode summary, curriculum block, HJ separation shift, goal_min_time, the
  * observation outputs) is the device's, as in lsm_reset. */
 int lsm_reset_layout(lsm_env* env, const lsm_curriculum* cur, const double* layout_device, void* hip_stream);
@@ -277,6 +282,15 @@ int lsm_buffer_insert(const float* obs, const uint8_t* dones, int32_t n, int32_t
                       int32_t centralized, float* share_obs, int32_t* agent_id, int32_t* share_agent_id,
                       float* masks, float* active_masks, void* hip_stream);
 const char* lsm_buffer_last_error(void);
+
+/* ---- Episode summary for the runner's log (lsm_metrics.hip) ---------------------------------
+ * Replaces the per-episode reduction of GMPERunner's ep-info parse (graph_mpe_runner.py:222-251:
+ * the mean over threads of the 8-key summaries, the min of min_distance_min). From one rank's
+ * ep_info [n][8] float64 (LSM_OUT_EP_INFO, 16-B aligned) it writes out[10] on the device, stream-
+ * ordered, no host sync: out[0..7] column sums, out[8] = n, out[9] = min of column 6 (NaN
+ * propagates). Across ranks out[0..8] is all_reduce(SUM)'d and out[9] all_reduce(MIN)'d (RCCL);
+ * mean = sum / count. Fixed addition order (reproducible). Nonzero on bad arguments. */
+int lsm_episode_summary(const double* ep_info, int32_t n, double* out /* [10] */, void* hip_stream);
 
 #ifdef __cplusplus
 }

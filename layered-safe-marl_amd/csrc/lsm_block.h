@@ -255,6 +255,9 @@ __global__ __launch_bounds__(BT) void rollout_block_kernel(const KParams* __rest
   // value only where the lower bound is <= U. A skipped pair's value exceeds U >= the minimum,
   // so the argmin (first occurrence on ties) and its value are exactly the full search's.
   const bool filter_on = S.cur[C_FILT] != 0.0;
+  // World.step's inner loop (core.py:607-631): filter -> action_diff -> integrate, num_internal_step
+  // times on the same raw actions
+  for (int it = 0; it < P.nis; ++it) {
   if (filter_on) {
     const SepChain sc = sep_chain(S.sep);
     const int i = tid / TE, q = tid - (tid / TE) * TE;
@@ -402,6 +405,7 @@ __global__ __launch_bounds__(BT) void rollout_block_kernel(const KParams* __rest
   // ---- 4. integrate ------------------------------------------------------------------------
   if (tid < N && !S.dpre[tid]) integrate_agent<DYN>(P, S, N, tid);
   __syncthreads();
+  }
   STAMP(5);
   if (P.o.cforce && tid < N) {   // optional contact forces (collision_force_agent)
     double fx, fy;

@@ -145,6 +145,7 @@ struct KParams {
   int filter_search; // workgroup kernel's HJ argmin: 1 bound-pruned (default), 0 every pair exact
   int scenario;      // LSM_SCENARIO_*
   int rng;           // LSM_RNG_*
+  int nis;           // World.num_internal_step (>= 1): filter -> integrate repeats per step
   int64_t seed, env_offset;   // Philox keys: seed + 1000 * (env_offset + env)
   uint32_t lds_dep_off;       // LSM_SCENARIO_DEPARTURES: LDS offset of the departure arrays
   double dt, world_size, coord_range, world_eng, sep_target, max_speed, min_speed, gs_min, gs_max;
@@ -826,9 +827,17 @@ __device__ __forceinline__ bool inactive_pre(const Lds& S, int j) {
   return S.dpre[j] || (S.dep0 && !S.dep0[j]);
 }
 
+// freeze_agent (navigation_graph_safe.py:1091-1099) runs when an agent BECOMES done
+// (update_reached_goal_and_done, :658-675): this step's transition. An agent done before the step
+// already holds its frozen state in the record (zeroed velocity, or -- scenario_circular_config's
+// kept-done agents -- the layout's state, which the reference never freezes again).
+__device__ __forceinline__ bool froze_now(const Lds& S, int j) {
+  return S.dpost[j] && !S.dpre[j];
+}
+
 template <int DYN>
 __device__ __forceinline__ void agent_vel(const Lds& S, int N, int j, bool post, double& vx, double& vy) {
-  const bool frozen = post && S.dpost[j];
+  const bool frozen = post && froze_now(S, j);
   if (DYN == 1 && post && S.psp) {   // departures: the post state carries departure / freezes
     const double th = S.pth[j], sp = S.psp[j];
     vx = sp * cos(th);
@@ -848,7 +857,7 @@ __device__ __forceinline__ void agent_vel(const Lds& S, int N, int j, bool post,
 
 template <int DYN>
 __device__ __forceinline__ double agent_speed(const Lds& S, int N, int j, bool post) {
-  const bool frozen = post && S.dpost[j];
+  const bool frozen = post && froze_now(S, j);
   if (DYN == 1 && post && S.psp) return S.psp[j];
   if (DYN == 0) {
     const double vx = frozen ? 0.0 : S.ps[2 * N + j];
@@ -1194,11 +1203,11 @@ __device__ __forceinline__ void node_features(const KParams& P, const Lds& S, in
   const double* tvy1 = dm ? S.trig1 + 3 * N : tvy;
   const double pex = S.ps[e], pey = S.ps[N + e];
   const double c = tc1[e], s = ts1[e];
-  const bool efz = !dm && S.dpost[e] != 0;     // the ego is seen after its own update
+  const bool efz = !dm && froze_now(S, e);     // the ego is seen after its own update
   const double vex = efz ? 0.0 : tvx1[e], vey = efz ? 0.0 : tvy1[e];
   if (k < N) {
     const bool post = k <= e;
-    const bool kfz = !dm && post && S.dpost[k];
+    const bool kfz = !dm && post && froze_now(S, k);
     const double vkx = kfz ? 0.0 : (post ? tvx1 : tvx)[k], vky = kfz ? 0.0 : (post ? tvy1 : tvy)[k];
     const double ck = (post ? tc1 : tc)[k], sk = (post ? ts1 : ts)[k];
     const int gi = goal_index(post ? S.rpost[k] : S.rpre[k], k, N, NL);
@@ -1292,7 +1301,7 @@ __device__ __forceinline__ void build_rows_di(const KParams& P, Lds& S) {
     if (t < 2 * N) {
       const bool post = t >= N;
       const int k = post ? t - N : t;
-      const bool frozen = post && dpost[k];
+      const bool frozen = post && dpost[k] && !S.dpre[k];
       const double vx = frozen ? 0.0 : S.ps[2 * N + k], vy = frozen ? 0.0 : S.ps[3 * N + k];
       const int gi = goal_index(post ? rpost[k] : S.rpre[k], k, N, NL);
       r[0] = S.ps[k]; r[1] = S.ps[N + k]; r[2] = vx; r[3] = vy;
@@ -1307,7 +1316,7 @@ __device__ __forceinline__ void build_rows_di(const KParams& P, Lds& S) {
   }
   if (lane < N) {
     const int e = lane;
-    const bool frozen = dpost[e] != 0;
+    const bool frozen = froze_now(S, e);
     const double vx = frozen ? 0.0 : S.ps[2 * N + e], vy = frozen ? 0.0 : S.ps[3 * N + e];
     double* o = S.egooff + e * F;
     o[0] = S.ps[e]; o[1] = S.ps[N + e]; o[2] = vx; o[3] = vy; o[4] = S.ps[e]; o[5] = S.ps[N + e];
@@ -1780,14 +1789,16 @@ __device__ __forceinline__ void reset_core(const KParams& P, Lds& S, int env, co
       S.sep[1] = cur_new[C_SEP];
     }
   }
+  bool keep_done = false;   // scenario_circular_config leaves done agents done (see below)
   ScenarioParams sp;
   sp.dyn = DYN; sp.N = N; sp.L = L; sp.world_size = P.world_size; sp.coordination_range = P.coord_range;
   sp.goal_speed_min = P.gs_min; sp.goal_speed_max = P.gs_max;
   sp.ratio_airtaxi = S.cur[C_RAT]; sp.ratio_scenario = S.cur[C_RSC]; sp.two_pi = P.two_pi; sp.pi = P.pi;
   if (layout) {
     // lsm_reset_layout: the host's evaluation layout replaces random_scenario (no device draws)
-    const int LD = 4 * N + 4 * NL + (S.dep0 ? 3 * N : 0);
+    const int LD = 4 * N + 4 * NL + (S.dep0 ? 3 * N : 0) + 1;   // last word: keep done
     const GAS double* g = gptr(layout) + (size_t)env * LD;
+    keep_done = g[LD - 1] != 0.0;
     for (int k = lane; k < 4 * N; k += LPE) {
       const int i = k >> 2, c = k & 3;
       S.ps[c * N + i] = g[k];
@@ -1851,7 +1862,10 @@ __device__ __forceinline__ void reset_core(const KParams& P, Lds& S, int env, co
     S.lmsc[NL + k] = cos(S.lm[2 * NL + k]);
   }
   for (int k = lane; k < N; k += LPE) {
-    S.dpre[k] = 0; S.dpost[k] = 0; S.rpre[k] = 0; S.rpost[k] = 0;
+    // every layout sets agent.done = False except scenario_circular_config (navigation_graph_safe_
+    // eval.py:100-121): there a done agent stays done, with the layout's state as its frozen state
+    const int32_t d = keep_done ? S.dpost[k] : 0;
+    S.dpre[k] = d; S.dpost[k] = d; S.rpre[k] = 0; S.rpost[k] = 0;
     S.emask[k] = 0;
     S.winfo[k] = -1.0; S.winfo[N + k] = -1.0; S.winfo[2 * N + k] = -1.0; S.winfo[3 * N + k] = 0.0;
     for (int q = 0; q < NSTAT; ++q) S.stats[q * N + k] = (q == 4) ? INFINITY : 0.0;
@@ -1860,11 +1874,14 @@ __device__ __forceinline__ void reset_core(const KParams& P, Lds& S, int env, co
   }
   if (lane == 0) { S.step[0] = 0; S.step[1] = 0; }
   esync<LPE>();   // MT words read out of U1 before compute_dist overwrites it
-  if (S.dep0) {
-    // departures: undeparted agents are disconnected from the reset's graph observation too
+  if (S.dep0 || keep_done) {
+    // departures: undeparted agents are disconnected from the reset's graph observation too;
+    // kept-done agents are disconnected as done
     for (int k = lane; k < N; k += LPE) {
-      S.pth[k] = S.ps[2 * N + k];
-      S.psp[k] = S.ps[3 * N + k];
+      if (S.dep0) {
+        S.pth[k] = S.ps[2 * N + k];
+        S.psp[k] = S.ps[3 * N + k];
+      }
       S.emask[k] = ego_mask(S, N, L, k);
     }
     esync<LPE>();
@@ -1925,7 +1942,7 @@ __device__ __forceinline__ void store_state(const KParams& P, Lds& S, const unsi
   for (int k = lane; k < 4 * N; k += LPE) {
     const int c = k / N, j = k - c * N;
     double v = S.ps[k];
-    if (S.dpost[j] && (DYN == 0 ? (c >= 2) : (c == 3))) v = 0.0;
+    if (froze_now(S, j) && (DYN == 0 ? (c >= 2) : (c == 3))) v = 0.0;
     S.ps[k] = v;
     if (P.o.state) gptr(P.o.state)[((size_t)env * N + j) * 4 + c] = v;
   }
@@ -2154,7 +2171,7 @@ __device__ __forceinline__ void info_agent(const KParams& P, Lds& S, int i, int 
     // departures: the update may have changed heading / speed (departure, freeze)
     reached_post = goal_reached_at<DYN>(S, N, NL, i, gi, S.psp[i], dae(S.pth[i], S.lm[2 * NL + gi]));
   } else if (S.rpost[i] != S.rpre[i]) {
-    const bool frz = S.dpost[i] != 0;
+    const bool frz = froze_now(S, i);
     const double spp = frz ? 0.0 : t.spd_pre;
     double hep;
     if (DYN == 0) {   // frozen: zero velocity, atan2(0, 0) = 0
@@ -2429,6 +2446,9 @@ __global__ __launch_bounds__(64, DYN == 0 ? (LPE == 64 ? 4 : 2) : LSM_WAVES_PER_
 #else
   const bool filter_on = S.cur[C_FILT] != 0.0;
 #endif
+  // World.step's inner loop (core.py:607-631): filter -> action_diff -> integrate, num_internal_step
+  // times on the same raw actions; the distances and min relative distance of the final state follow
+  for (int it = 0; it < P.nis; ++it) {
   if (filter_on) {
     const SepChain sc = sep_chain(S.sep);
     const int npairs = N * N;
@@ -2455,6 +2475,7 @@ __global__ __launch_bounds__(64, DYN == 0 ? (LPE == 64 ? 4 : 2) : LSM_WAVES_PER_
   // ---- 4. integrate ----------------------------------------------------------------------
   if (lane < N && !inactive_pre(S, lane)) integrate_agent<DYN>(P, S, N, lane);
   __syncthreads();
+  }
   STAMP(5);
 
   // ---- 5. distances, min relative distance ---------------------------------------------
@@ -2642,6 +2663,7 @@ static void fill_params(const lsm_env* e, KParams& P) {
   if (const char* v = getenv("LSM_FILTER_SEARCH")) P.filter_search = atoi(v);
   P.scenario = e->cfg.scenario;
   P.rng = e->cfg.rng;
+  P.nis = e->cfg.num_internal_step > 1 ? e->cfg.num_internal_step : 1;
   P.seed = e->cfg.seed;
   P.env_offset = e->cfg.env_offset;
   P.lds_dep_off = (uint32_t)lds_plan(e->N, e->NL, e->E, e->F, e->block).bytes;
@@ -2745,7 +2767,7 @@ size_t lsm_output_bytes(const lsm_env* e, int32_t slot) {
 
 int32_t lsm_num_entities(const lsm_env* e) { return e->E; }
 int32_t lsm_layout_doubles(const lsm_env* e) {
-  return e ? 4 * e->N + 4 * e->NL + (e->cfg.scenario == LSM_SCENARIO_DEPARTURES ? 3 * e->N : 0) : 0;
+  return e ? 4 * e->N + 4 * e->NL + (e->cfg.scenario == LSM_SCENARIO_DEPARTURES ? 3 * e->N : 0) + 1 : 0;
 }
 int32_t lsm_node_features(const lsm_env* e) { return e->F; }
 int32_t lsm_obs_dim(const lsm_env* e) { return e->OBS; }
@@ -2799,6 +2821,8 @@ int lsm_create(const lsm_config* cfg, lsm_env** out) {
     e->block = N > MAXN || N * (1 + L) > MAXE || (kv && strcmp(kv, "block") == 0);
   }
   if (cfg->num_envs < 1) return fail(e, "num_envs must be >= 1");
+  if (cfg->num_internal_step < 0 || cfg->num_internal_step > 64)
+    return fail(e, "num_internal_step must be in [0, 64] (0 and 1: one inner step)");
   if (cfg->episode_length < 1) return fail(e, "episode_length must be >= 1");
   e->N = N; e->L = L; e->NL = N * L; e->E = N * (1 + L);
   e->F = cfg->dynamics == LSM_DOUBLE_INTEGRATOR ? 10 : 11;
@@ -2818,7 +2842,9 @@ int lsm_create(const lsm_config* cfg, lsm_env** out) {
   // workgroup share one wave for their per-agent phases. LSM_TEAM=0 selects rollout_kernel,
   // LSM_TEAM=G another instantiated G.
   e->team = 0;
-  if (!e->block && e->lpe == 64 && L == 2 && !e->generic_only) {
+  // the team kernel runs World.step's inner loop once (num_internal_step = 1, the training
+  // default, train.sh:35); more inner steps run in rollout_kernel / the workgroup kernel
+  if (!e->block && e->lpe == 64 && L == 2 && !e->generic_only && cfg->num_internal_step <= 1) {
     if (cfg->dynamics == LSM_DOUBLE_INTEGRATOR && N == 8) e->team = 4;   // measured: 4 < 8 < 2 (us/step)
     if (cfg->dynamics == LSM_AIRTAXI && N == 16) e->team = 4;   // lean LDS: 4 < 2 < 0 (us/step)
     if (const char* v = getenv("LSM_TEAM")) {

@@ -18,6 +18,7 @@ UNITS = {
     "lsm_rollout.hip": ["lsm_numeric.h", "lsm_scenario.h", "lsm_block.h", "lsm_rk45.h", "lsm_pow_tables.h", "lsm_team.h"],
     "lsm_edges.hip": [],
     "lsm_buffer.hip": [],
+    "lsm_metrics.hip": [],
 }
 
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

@@ -35,7 +35,7 @@ EXPORTED = ("lsm_create", "lsm_destroy", "lsm_last_error", "lsm_set_value_table"
             "lsm_edges_last_error", "lsm_bind_output_ring", "lsm_select_ring", "lsm_buffer_insert",
             "lsm_buffer_last_error", "lsm_host_rk45_di", "lsm_host_glibc_pow", "lsm_action_errors",
             "lsm_kernel_name", "lsm_reset_layout", "lsm_layout_doubles", "lsm_host_philox_uniforms",
-            "lsm_host_philox4x32")
+            "lsm_host_philox4x32", "lsm_episode_summary")
 
 
 class LsmConfig(C.Structure):
@@ -45,7 +45,7 @@ class LsmConfig(C.Structure):
                 ("auto_reset", C.c_int32), ("emit_edges", C.c_int32), ("adj_layout", C.c_int32),
                 ("world_size", C.c_double), ("seed", C.c_int64), ("env_offset", C.c_int64),
                 ("collision_forces", C.c_int32), ("scenario", C.c_int32), ("rng", C.c_int32),
-                ("reserved1", C.c_int32)]
+                ("num_internal_step", C.c_int32)]
 
 
 class LsmCurriculum(C.Structure):
@@ -104,6 +104,7 @@ def load_library(path: str = LIB_PATH):
         "lsm_layout_doubles": (I32, [P]),
         "lsm_host_philox_uniforms": (I32, [U32, U32, I32, D, D, P]),
         "lsm_host_philox4x32": (I32, [P, P, P]),
+        "lsm_episode_summary": (I32, [P, I32, P, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

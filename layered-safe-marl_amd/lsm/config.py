@@ -150,8 +150,8 @@ class EnvArgs:
             raise ValueError("only graph_feat_type='relative' is on the path (train.sh)")
         if self.num_landmarks < 1 and self.scenario_name == "navigation_graph_safe":
             raise ValueError("num_landmarks must be >= 1")
-        if self.num_internal_step != 1:
-            raise ValueError("num_internal_step != 1 is not supported")
+        if not 1 <= int(self.num_internal_step) <= 64:
+            raise ValueError("num_internal_step must be in [1, 64] (World.step's inner loop, core.py:607)")
         if not self.discrete_action:
             raise ValueError("only the Discrete(25) action space is on the path")
         total = int(self.num_env_steps) // self.episode_length // self.n_rollout_threads

@@ -62,14 +62,26 @@ class EpisodeSummaryReducer:
         self.group = group
         self.device = torch.device(device)
         # the env count rides in the SUM buffer (one collective gives sums and the global count)
-        self._cnt = torch.full((1,), float(n_local), dtype=torch.float64, device=self.device)
+        self._cnt = torch.full((1,), float(n_local), dtype=torch.float64)
         self._pending = []
 
     def submit(self, ep_info: torch.Tensor):
-        buf = torch.empty(9, dtype=torch.float64, device=ep_info.device)
-        torch.sum(ep_info, dim=0, out=buf[:8])
-        buf[8:].copy_(self._cnt)
-        mn = torch.amin(ep_info[:, 6:7], dim=0)
+        out = torch.empty(10, dtype=torch.float64, device=ep_info.device)
+        if ep_info.is_cuda:
+            # one native launch (lsm_metrics.hip): sums, count, min -- no host sync
+            import ctypes as C
+            from . import capi
+            lib = capi.load_library()
+            ep = ep_info.contiguous()
+            st = torch.cuda.current_stream(ep.device).cuda_stream
+            if lib.lsm_episode_summary(C.c_void_p(ep.data_ptr()), int(ep.shape[0]), C.c_void_p(out.data_ptr()),
+                                       C.c_void_p(st)) != 0:
+                raise capi.LsmError("lsm_episode_summary failed")
+        else:   # host tensors (gloo tests on the CPU): the same sums with torch
+            torch.sum(ep_info, dim=0, out=out[:8])
+            out[8:9].copy_(self._cnt.to(out.device))
+            out[9:10] = torch.amin(ep_info[:, 6:7], dim=0)
+        buf, mn = out[:9], out[9:10]
         works = ()
         if _dist_on():
             import torch.distributed as dist

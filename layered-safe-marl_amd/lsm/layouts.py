@@ -101,8 +101,8 @@ class Layout:
     timer: Optional[np.ndarray] = None
     init_theta: Optional[np.ndarray] = None
     # every layout sets agent.done = False except circular_config (navigation_graph_safe_eval.py:
-    # 100-121), which leaves done agents of the previous episode done. The device reset clears
-    # done for every layout: a known divergence from that layout's second episode on.
+    # 100-121), which leaves done agents of the previous episode done (packed as the keep-done
+    # word the device reset honours, include/lsm_rollout.h lsm_reset_layout)
     clears_done: bool = True
 
     def pack(self) -> np.ndarray:
@@ -110,6 +110,7 @@ class Layout:
         if self.departed is not None:
             parts += [self.departed.astype(np.float64), self.timer.astype(np.float64),
                       self.init_theta.astype(np.float64)]
+        parts.append(np.array([0.0 if self.clears_done else 1.0]))
         return np.concatenate(parts)
 
 
@@ -175,11 +176,12 @@ class ScenarioLayout:
 
     def _landmarks(self, pos, head, speed):
         lm = np.zeros((self.NL, 4))
-        # the reference assigns world.landmarks[k] for k < N * L from these lists (the cross
-        # layout's speed lists are longer: 7 per agent for 6 landmarks, all equal)
-        if len(pos) != self.NL or len(head) < self.NL or len(speed) < self.NL:
-            raise ValueError("layout has %d landmarks, the env %d (num_landmarks per agent = %d)"
-                             % (len(pos), self.NL, self.L))
+        # the reference assigns world.landmarks[k] for k < N * L from these (order-major) lists:
+        # longer lists are truncated -- e.g. a Bay Area map run with a smaller --num_landmarks
+        # keeps each agent's first L waypoints -- and shorter ones raise its IndexError
+        if len(pos) < self.NL or len(head) < self.NL or len(speed) < self.NL:
+            raise ValueError("layout has %d landmarks, the env %d (num_landmarks per agent = %d): the "
+                             "reference raises IndexError" % (len(pos), self.NL, self.L))
         for k in range(self.NL):
             lm[k, 0:2] = pos[k]
             lm[k, 2] = head[k]
@@ -336,8 +338,6 @@ class ScenarioLayout:
         if self.N != len(depart) * len(goals):
             raise ValueError("Number of agents should be equal to the product of number of depart positions and "
                              "goal positions (8)")
-        if self.L != 5:
-            raise ValueError("city_inbound places 5 landmarks per agent")
         dep = np.zeros(self.N)
         tmr = np.zeros(self.N)
         ith = np.zeros(self.N)
@@ -386,8 +386,6 @@ class ScenarioLayout:
         c2 = [(1569, 908), (1556, 1320), (1536, 1692), (1536, 2048), (1535, 2420), (1535, 2764)]
         if self.N % 2:
             raise ValueError("Number of agents should be even")
-        if self.L != 6:
-            raise ValueError("fixed_schedule places 6 landmarks per agent")
         depart = [self.px(c1[0]), self.px(c2[0])]
         w1 = [self.px(w) for w in c1][1:]
         last1 = np.arctan2(w1[-1][1] - w1[-2][1], w1[-1][0] - w1[-2][0])

@@ -149,7 +149,8 @@ class GpuGraphVecEnv(ShareVecEnv):
                              seed=int(a.seed), env_offset=int(env_offset),
                              collision_forces=int(bool(collision_forces)),
                              scenario=layout.scenario_code if layout is not None else capi.LSM_SCENARIO_TRAIN,
-                             rng=capi.LSM_RNG_PHILOX if rng == "philox" else capi.LSM_RNG_MT19937)
+                             rng=capi.LSM_RNG_PHILOX if rng == "philox" else capi.LSM_RNG_MT19937,
+                             num_internal_step=int(a.num_internal_step))
         if int(a.seed) + 1000 * (int(env_offset) + self.num_envs - 1) >= 2 ** 32:
             raise ValueError("numpy seeds must be < 2**32 (seed + 1000 * env index)")
         h = C.c_void_p()

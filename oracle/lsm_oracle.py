@@ -181,6 +181,7 @@ class OracleEnv:
         self.C = _DI if self.di else _AT
         self.integrator = integrator
         self.report_collision_forces = bool(g("collision_forces", False))
+        self.num_internal_step = max(1, int(g("num_internal_step", 1) or 1))   # World.step inner loop
         self.cforce = np.zeros((self.N, 2))
         C = self.C
         self.dt = C.DT
@@ -847,6 +848,25 @@ class OracleEnv:
         return u
 
     def world_step(self, raw):
+        """World.step (core.py:593-631): num_internal_step x (filter -> action_diff -> integrate),
+        then the distances and the minimum relative distance of the final state."""
+        for _ in range(self.num_internal_step):
+            self._inner_step(raw)
+        self.calculate_distances()
+        if self.report_collision_forces:
+            self.cforce = self.collision_forces()
+        M = np.inf * np.ones((self.N, self.N))
+        for i in range(self.N):
+            if self.done[i] or not self.departed[i]:
+                continue
+            for j in range(self.N):
+                if i == j or not self.departed[j] or self.done[j]:
+                    continue
+                M[i, j] = np.linalg.norm(self.pos(i) - self.pos(j))
+        for i in range(self.N):
+            self.min_rel_dist[i] = np.min(M[i, :])
+
+    def _inner_step(self, raw):
         if self.world_filter_on:
             safe, flags, dec = [], [], []
             for i in range(self.N):
@@ -866,19 +886,6 @@ class OracleEnv:
             if self.done[i] or not self.departed[i]:
                 continue
             self._integrate(i, safe[i])
-        self.calculate_distances()
-        if self.report_collision_forces:
-            self.cforce = self.collision_forces()
-        M = np.inf * np.ones((self.N, self.N))
-        for i in range(self.N):
-            if self.done[i] or not self.departed[i]:
-                continue
-            for j in range(self.N):
-                if i == j or not self.departed[j] or self.done[j]:
-                    continue
-                M[i, j] = np.linalg.norm(self.pos(i) - self.pos(j))
-        for i in range(self.N):
-            self.min_rel_dist[i] = np.min(M[i, :])
         self._safe = safe
 
     def info(self, i):

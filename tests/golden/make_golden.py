@@ -318,8 +318,8 @@ def main(only=None):
         lambda: run_case("ev_at_circ_n4", A(scenario_name="navigation_graph_safe_eval", num_agents=4,
                                             num_landmarks=0, num_env_steps=120 * 4, dynamics_type="airtaxi",
                                             world_size=6, episode_length=120, use_safety_filter=True),
-                         seed=33, ep=4, steps=120, value_stored=at_small, ttr_stored=ttr_small,
-                         action_seed=12, eval_type="circular_config", dummy=True),
+                         seed=33, ep=4, steps=240, value_stored=at_small, ttr_stored=ttr_small,
+                         action_seed=12, eval_type="circular_config", dummy=True),   # 2 episodes: kept done
         lambda: run_case("ev_at_conflict3", A(scenario_name="navigation_graph_safe_eval", num_agents=3,
                                               num_landmarks=0, num_env_steps=80 * 4, dynamics_type="airtaxi",
                                               world_size=6, episode_length=80, use_safety_filter=True),
@@ -336,12 +336,41 @@ def main(only=None):
                          seed=36, ep=4, steps=380, value_stored=at_small, ttr_stored=ttr_small,
                          action_seed=15, image_size=(3300, 3000), dummy=True),
     ]
+    # a Bay Area map run with a smaller --num_landmarks than its waypoint lists: the reference
+    # assigns world.landmarks[k] for k < N * L, i.e. keeps each agent's first L waypoints
+    merge_l3 = lambda: run_case("ba_merge_n8_l3", A(scenario_name="navigation_graph_safe_bayarea_merge", num_agents=8,
+                                                    num_landmarks=3, num_env_steps=100 * 4, dynamics_type="airtaxi",
+                                                    episode_length=100, use_safety_filter=True),
+                                seed=37, ep=4, steps=200, value_stored=at_small, ttr_stored=ttr_small,
+                                action_seed=16, image_size=(2400, 2000), dummy=True)
     if only == "layouts":
         for f in layouts:
             f()
+        merge_l3()
         return
     if only == "ba_cross":
         layouts[-1]()
+        return
+    if only == "circ":
+        layouts[2]()
+        return
+    if only == "ba_merge_l3":
+        merge_l3()
+        return
+    # World.step's inner loop (core.py:607-631) run num_internal_step times per env step
+    nis = [
+        lambda: run_case("di_n4_nis2", A(num_agents=4, num_env_steps=60 * 4, episode_length=60, use_safety_filter=True,
+                                         num_internal_step=2), seed=43, ep=4, steps=130, value_stored=di_small,
+                         action_seed=17),
+        lambda: run_case("at_n3_nis3", A(num_agents=3, num_env_steps=60 * 4, dynamics_type="airtaxi", world_size=6,
+                                         episode_length=60, use_safety_filter=True, num_internal_step=3),
+                         seed=44, ep=4, steps=80, value_stored=at_small, ttr_stored=ttr_small, action_seed=18),
+        lambda: run_case("di_n3_off_nis3", A(num_agents=3, num_env_steps=60 * 4, episode_length=60,
+                                             num_internal_step=3), seed=45, ep=1, steps=70, action_seed=19),
+    ]
+    if only == "nis":
+        for f in nis:
+            f()
         return
     if only == "collision":
         record_collision_forces()

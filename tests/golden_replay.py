@@ -25,11 +25,12 @@ LAYOUT_PREFIXES = ("ev_", "ba_")
 
 
 def fixture_names():
-    """The training-scenario rollout fixtures (each holds a "meta" record); collision_forces.npz is
-    a function-level fixture of its own (tests/test_collision_forces.py), the evaluation-layout
+    """The training-scenario rollout fixtures (each holds a "meta" record); collision_forces.npz and
+    runner_metrics.npz are function-level fixtures of their own (tests/test_collision_forces.py,
+    tests/test_metrics.py), the evaluation-layout
     fixtures are listed by layout_fixture_names()."""
     return sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, "*.npz"))
-                  if not os.path.basename(p).startswith(("collision",) + LAYOUT_PREFIXES))
+                  if not os.path.basename(p).startswith(("collision", "runner") + LAYOUT_PREFIXES))
 
 
 def layout_fixture_names():

@@ -58,3 +58,78 @@ def test_gpu_metrics_match_reference_restatement(dyn, n_agents, filt):
             np.testing.assert_allclose(means[k], np.mean(v), rtol=tol, atol=tol, err_msg="step %d %s" % (t, k))
     assert isinstance(env.t_info, torch.Tensor) and env.t_info.is_cuda
     env.close()
+
+
+@pytest.mark.parametrize("n", [0, 1, 255, 4096, 8195])
+def test_gpu_episode_summary_kernel(n):
+    """lsm_episode_summary (one launch, no host sync) equals the column sums, the count and the
+    NaN-propagating min of min_distance_min that GMPERunner's parse reduces (graph_mpe_runner.py:
+    222-251); EpisodeSummaryReducer's means equal numpy's."""
+    import ctypes as C
+    import torch
+    from lsm import capi
+    from lsm.dist import EPKEYS, EpisodeSummaryReducer
+    lib = capi.load_library()
+    rng = np.random.default_rng(n)
+    ep = rng.uniform(-3, 10, (n, 8))
+    ep[:, 6] = rng.uniform(0.01, 4.0, n)
+    t = torch.tensor(ep, dtype=torch.float64, device="cuda:0")
+    out = torch.full((10,), -7.0, dtype=torch.float64, device="cuda:0")
+    st = torch.cuda.current_stream().cuda_stream
+    assert lib.lsm_episode_summary(C.c_void_p(t.data_ptr()), n, C.c_void_p(out.data_ptr()), C.c_void_p(st)) == 0
+    o = out.cpu().numpy()
+    np.testing.assert_allclose(o[:8], ep.sum(axis=0), rtol=1e-13, atol=1e-12)
+    assert o[8] == n
+    assert o[9] == (ep[:, 6].min() if n else np.inf)
+    if n:
+        r = EpisodeSummaryReducer(n, "cuda:0")
+        r.submit(t)
+        r.submit(t)
+        got = r.results()
+        assert len(got) == 2 and got[0] == got[1]
+        want = ep.mean(axis=0)
+        want[6] = ep[:, 6].min()
+        np.testing.assert_allclose([got[0][k] for k in EPKEYS], want, rtol=1e-12, atol=1e-12)
+        ep[n // 2, 6] = np.nan
+        t = torch.tensor(ep, dtype=torch.float64, device="cuda:0")
+        lib.lsm_episode_summary(C.c_void_p(t.data_ptr()), n, C.c_void_p(out.data_ptr()), C.c_void_p(st))
+        assert np.isnan(out[9].item())
+
+
+def test_gpu_metrics_match_reference_runner_functions():
+    """Pinned to the reference's own functions: tests/golden/runner_metrics.npz holds what
+    Runner.process_infos / log_env (base_runner.py:222-331) returned on K reference envs
+    (make_runner_metrics.py). A device handle with the same seeds and actions, through
+    lsm.metrics on its info tensor, gives the same per-env lists and log means every step across
+    the auto-reset (rtol 1e-9; individual rewards -- float32 outputs -- 1e-5)."""
+    import ast
+    import os
+    from golden_replay import tables_for
+    from lsm import metrics
+    from lsm.config import EnvArgs
+    from lsm.vec_env import GpuGraphVecEnv
+    z = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "runner_metrics.npz"))
+    m = ast.literal_eval(str(z["meta"]))
+    vt, _ = tables_for(m)
+    args = EnvArgs(dynamics_type=m["dynamics_type"], num_agents=m["num_agents"], world_size=m["world_size"],
+                   episode_length=m["episode_length"], num_env_steps=m["num_env_steps"], use_safety_filter=True,
+                   seed=m["seed"])
+    env = GpuGraphVecEnv(args, num_envs=m["n_envs"], device="cuda:0", value_table=vt, return_numpy=False)
+    env.reset(m["ep"])
+    keys = [str(k) for k in z["keys"]]
+    log_keys = [str(k) for k in z["log_keys"]]
+    N, L, dt = m["num_agents"], m["episode_length"], m["dt"]
+    for t in range(len(z["act"])):
+        env.step(z["act"][t], m["ep"])
+        got = metrics.process_infos(env.t_info, N, L, dt)
+        assert sorted(got) == keys
+        means = metrics.log_means(env.t_info, N, L, dt)
+        assert sorted(means) == log_keys
+        for i, k in enumerate(keys):
+            want = z["vals"][t, i, :int(z["lens"][i])]
+            tol = 1e-5 if k.endswith("individual_rewards") else 1e-9
+            np.testing.assert_allclose(got[k], want, rtol=tol, atol=tol, err_msg="step %d %s" % (t, k))
+        for j, k in enumerate(log_keys):
+            tol = 1e-5 if k.endswith("individual_rewards") else 1e-9
+            np.testing.assert_allclose(means[k], z["log_vals"][t, j], rtol=tol, atol=tol, err_msg="step %d %s" % (t, k))
+    env.close()

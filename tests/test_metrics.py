@@ -89,3 +89,45 @@ def test_log_means_on_device_tensor():
             assert k not in got
             continue
         np.testing.assert_allclose(got[k], np.mean(v), rtol=1e-12, atol=1e-12, err_msg=k)
+
+
+def _runner_fixture():
+    import ast
+    import os
+    z = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "runner_metrics.npz"))
+    return z, ast.literal_eval(str(z["meta"]))
+
+
+def _fixture_lists(z, t):
+    out = {}
+    for i, k in enumerate(z["keys"]):
+        out[str(k)] = [float(x) for x in z["vals"][t, i, :int(z["lens"][i])]]
+    return out
+
+
+def test_restatement_and_oracle_match_reference_runner_functions():
+    """Pinned to the reference: tests/golden/runner_metrics.npz holds Runner.process_infos /
+    log_env outputs (base_runner.py:222-331) recorded from the stub-imported reference on K
+    reference envs. The oracle's info dicts for the same seeds and actions, through the
+    restatement above and np.mean, give the same dicts and means, every step, across the
+    auto-reset."""
+    from golden_replay import table_dict, tables_for
+    from oracle.lsm_oracle import OracleVecEnv
+    z, m = _runner_fixture()
+    vt, _ = tables_for(m)
+    meta = dict(dynamics_type=m["dynamics_type"], num_agents=m["num_agents"], num_landmarks=2,
+                world_size=m["world_size"], episode_length=m["episode_length"], num_env_steps=m["num_env_steps"],
+                n_rollout_threads=1, use_safety_filter=True, use_masking=True, num_internal_step=1)
+    ora = OracleVecEnv(meta, m["n_envs"], seed=m["seed"], value_table=table_dict(vt), integrator="rk45")
+    ora.reset(m["ep"])
+    log_keys = [str(k) for k in z["log_keys"]]
+    for t in range(len(z["act"])):
+        *_, infos = ora.step(z["act"][t], m["ep"])
+        got = _reference_process_infos(infos, m["num_agents"], m["episode_length"], m["dt"])
+        want = _fixture_lists(z, t)
+        assert set(got) == set(want)
+        for k in want:
+            np.testing.assert_allclose(got[k], want[k], rtol=1e-12, atol=1e-12, err_msg="step %d %s" % (t, k))
+        means = {k: np.mean(v) for k, v in got.items() if len(v) > 0}
+        assert sorted(means) == sorted(log_keys)
+        np.testing.assert_allclose([means[k] for k in log_keys], z["log_vals"][t], rtol=1e-12, atol=1e-12)
