@@ -26,12 +26,13 @@ __host__ __device__ constexpr int block_tpe(int N) {
 
 __device__ __forceinline__ bool mbit(const uint64_t* m, int k) { return (m[k >> 6] >> (k & 63)) & 1ull; }
 
-// entity k disconnected (navigation_graph_safe.py:976-989): a done agent, or landmark
-// l = o * N + j already reached by its agent j (reached_goal[j] > o)
+// entity k disconnected (navigation_graph_safe.py:976-989): a done or (RealisticScenario) not
+// yet departed agent, or landmark l = o * N + j already reached by its agent j (reached_goal[j] > o)
 template <bool POST>
 __device__ __forceinline__ bool entity_disc(const Lds& S, int N, int E, int k) {
   if (k >= E) return false;
-  if (k < N) return (POST ? S.dpost[k] : S.dpre[k]) != 0;
+  if (k < N)
+    return (POST ? S.dpost[k] : S.dpre[k]) != 0 || (S.dep0 && !(POST ? S.dep1[k] : S.dep0[k]));
   const int l = k - N, o = l / N, j = l - o * N;
   return (POST ? S.rpost[j] : S.rpre[j]) > o;
 }
@@ -110,7 +111,10 @@ __device__ __forceinline__ void emit_graph_block(const KParams& P, Lds& S, int e
   LSM_DIMS;
   const int MW = (E + 63) >> 6;
   if (DYN == 0) build_rows_di<BT, NT>(P, S); else trig_table_at<BT, NT>(P, S);
-  const bool uni = __syncthreads_and(tid >= N || (S.dpre[tid] == S.dpost[tid] && S.rpre[tid] == S.rpost[tid]));
+  // departures: per-ego masks and post rows differ by the accumulation rule even without a status
+  // change (the one-wave kernel's emit_graph does the same)
+  const bool uni = __syncthreads_and(tid >= N || (S.dpre[tid] == S.dpost[tid] && S.rpre[tid] == S.rpost[tid])) &&
+                   !S.dep0;
   const int EE = E * E;
   if (P.adj_compact) {
     GAS float* a = gptr(P.o.adj) + (size_t)env * EE;
@@ -165,12 +169,17 @@ __device__ __forceinline__ void emit_graph_block(const KParams& P, Lds& S, int e
 }
 
 template <int DYN, int NT>
-__device__ __forceinline__ void reset_block(const KParams& P, Lds& S, int env, const double* cur_new) {
+__device__ __forceinline__ void reset_block(const KParams& P, Lds& S, int env, const double* cur_new,
+                                            const double* layout = nullptr) {
   const int tid = threadIdx.x;
   LSM_DIMS;
-  reset_core<DYN, BT, NT>(P, S, env, cur_new);   // ends with a barrier
+  reset_core<DYN, BT, NT>(P, S, env, cur_new, layout);   // ends with a barrier
   const int MW = (E + 63) >> 6;
-  for (int k = tid; k < N * MW; k += BT) S.emask[k] = 0ull;
+  // the reset's disconnect masks: nothing in the training scenario; undeparted agents
+  // (RealisticScenario) and circular_config's kept-done agents in a layout (pre == post here)
+  mask_words(S, N, E);
+  __syncthreads();
+  for (int k = tid; k < N * MW; k += BT) S.emask[k] = S.mpost[k % MW];
   entity_table<NT>(P, S);
   if (tid < N) write_obs<DYN, NT>(P, S, env, tid);
   __syncthreads();
@@ -190,6 +199,8 @@ __global__ __launch_bounds__(BT) void rollout_block_kernel(const KParams* __rest
   constexpr int T = NT ? block_tpe(NT) : 64;      // butterfly bound (generic: up to 64 lanes)
   const int TE = NT ? T : block_tpe(N);           // threads per ego actually used
   Lds S = carve_block(smem, N, NL, E, F);
+  // RealisticScenario departure arrays (airtaxi layouts; the Bay Area intersection at 16 agents)
+  if (DYN == 1 && NT == 0 && P.scenario == LSM_SCENARIO_DEPARTURES) carve_dep(S, smem, P.lds_dep_off, N);
   RTSTAMP(13);
 #ifdef LSM_STAMPS
   if (tid == 0 && gptr(P.stamps))
@@ -209,13 +220,21 @@ __global__ __launch_bounds__(BT) void rollout_block_kernel(const KParams* __rest
       S.ecs[tid] = cos(S.ps[2 * N + tid]);
       S.ecs[N + tid] = sin(S.ps[2 * N + tid]);
     }
+    if (S.dep0 && K.mode == 0) {
+      const GAS double* dg = gptr(P.s.dep) + (size_t)env * depw(N);
+      S.dep0[tid] = S.dep1[tid] = dg[tid] != 0.0;
+      S.tmr[tid] = (int32_t)dg[N + tid];
+      S.ith[tid] = dg[2 * N + tid];
+      S.pth[tid] = S.ps[2 * N + tid];
+      S.psp[tid] = S.ps[3 * N + tid];
+    }
   }
   const int cstep = S.step[0] + 1;
   __syncthreads();
   STAMP(1);
 
-  if (K.mode == 1) {
-    reset_block<DYN, NT>(P, S, env, K.cur_new);
+  if (K.mode != 0) {   // 1: device scenario, 2: host layout (lsm_reset_layout)
+    reset_block<DYN, NT>(P, S, env, K.cur_new, K.mode == 2 ? K.layout : nullptr);
     __syncthreads();
     store_state<DYN, BT, NT>(P, S, smem, env, true);
     return;
@@ -226,8 +245,13 @@ __global__ __launch_bounds__(BT) void rollout_block_kernel(const KParams* __rest
     entity_table<NT>(P, S);
     mask_words(S, N, E);
     __syncthreads();
-    GAS uint8_t* eo = gptr(P.o.edges) + (size_t)env * E * E;
     const bool fresh = S.step[1] != 0;   // lsm_set_agent_state: calculate_distances() unmasked
+    if (S.dep0 && !fresh) {
+      // departures: the last ego's accumulated mask of the previous step, as stored
+      if (tid < MW) S.mpost[tid] = ((const GAS uint64_t*)(gptr(P.s.dep) + (size_t)env * depw(N) + 3 * N))[tid];
+      __syncthreads();
+    }
+    GAS uint8_t* eo = gptr(P.o.edges) + (size_t)env * E * E;
     for (int u = tid; u < E * E; u += BT) {
       const int a = qdiv<NT>(u, E, P.m_E), b = u - a * E;
       const double dx = S.ex[a] - S.ex[b], dy = S.ey[a] - S.ey[b];
@@ -264,7 +288,7 @@ __global__ __launch_bounds__(BT) void rollout_block_kernel(const KParams* __rest
     int jd = -1, jv = -1, okv = 0;
     double dmin = 0.0;
     float vmin = 0.0f;
-    const bool ego = i < N && !S.dpre[i];
+    const bool ego = i < N && !inactive_pre(S, i);
     constexpr int JN = NT ? (NT + T - 1) / T : 0;   // pairs per thread (compile-time N)
     if (JN > 0 && P.filter_search == 1) {
       // pass 1: bounds of every pair, loads issued together (slots unrolled)
@@ -274,7 +298,7 @@ __global__ __launch_bounds__(BT) void rollout_block_kernel(const KParams* __rest
       for (int k = 0; k < JN; ++k) {
         const int j = q + k * TE;
         lbk[k] = INFINITY;
-        if (ego && j < N && j != i && !S.dpre[j]) {
+        if (ego && j < N && j != i && !inactive_pre(S, j)) {
           const double ex = S.ps[i], ey = S.ps[N + i], ox = S.ps[j], oy = S.ps[N + j];
           const double d = sqrt((ox - ex) * (ox - ex) + (oy - ey) * (oy - ey));
           if (jd < 0 || d < dmin) { jd = j; dmin = d; }
@@ -355,7 +379,7 @@ __global__ __launch_bounds__(BT) void rollout_block_kernel(const KParams* __rest
       if (ego) {
 #pragma unroll 4
         for (int j = q; j < N; j += TE) {
-          if (j == i || S.dpre[j]) continue;
+          if (j == i || inactive_pre(S, j)) continue;
           const double ex = S.ps[i], ey = S.ps[N + i], ox = S.ps[j], oy = S.ps[N + j];
           const double d = sqrt((ox - ex) * (ox - ex) + (oy - ey) * (oy - ey));
           double rel[5];
@@ -403,8 +427,15 @@ __global__ __launch_bounds__(BT) void rollout_block_kernel(const KParams* __rest
   STAMP(4);
 
   // ---- 4. integrate ------------------------------------------------------------------------
-  if (tid < N && !S.dpre[tid]) integrate_agent<DYN>(P, S, N, tid);
+  if (tid < N && !inactive_pre(S, tid)) integrate_agent<DYN>(P, S, N, tid);
   __syncthreads();
+  if (DYN == 1 && it + 1 < P.nis) {   // the next inner filter's ego frame: the new headings
+    if (tid < N) {
+      S.ecs[tid] = cos(S.ps[2 * N + tid]);
+      S.ecs[N + tid] = sin(S.ps[2 * N + tid]);
+    }
+    __syncthreads();
+  }
   }
   STAMP(5);
   if (P.o.cforce && tid < N) {   // optional contact forces (collision_force_agent)
@@ -422,12 +453,12 @@ __global__ __launch_bounds__(BT) void rollout_block_kernel(const KParams* __rest
     double m = INFINITY;
     int cc = 0;
     if (i < N) {
-      const bool iact = !S.dpre[i];
+      const bool iact = !inactive_pre(S, i);
 #pragma unroll 4
       for (int j = q; j < N; j += TE) {
         if (j == i) continue;
         const double d2 = blas_norm2(S.ps[i] - S.ps[j], S.ps[N + i] - S.ps[N + j]);
-        if (iact && !S.dpre[j]) m = (d2 < m) ? d2 : m;
+        if (iact && !inactive_pre(S, j)) m = (d2 < m) ? d2 : m;
         if (d2 < 1.05 * (0.05 + 0.05)) cc++;
       }
     }
@@ -456,7 +487,15 @@ __global__ __launch_bounds__(BT) void rollout_block_kernel(const KParams* __rest
   for (int k = tid; k < N * MW; k += BT) {
     const int e = k / MW, w = k - e * MW;
     const uint64_t sel = post_sel(N, L, e, w);
-    S.emask[k] = (S.mpost[w] & sel) | (S.mpre[w] & ~sel);
+    uint64_t m = (S.mpost[w] & sel) | (S.mpre[w] & ~sel);
+    if (S.dep0 && w == 0) {
+      // graph_observation masks cached_dist_mag IN PLACE (navigation_graph_safe.py:986-987): a
+      // departure connects, so agent j >= 1 undeparted before the update was masked by ego 0 and
+      // stays masked for every later ego of this step (agents are entities 0..N-1 <= 63: word 0)
+      for (int j = 1; j < N; ++j)
+        if (!S.dep0[j]) m |= 1ull << j;
+    }
+    S.emask[k] = m;
   }
   STAMP(7);
 
@@ -474,7 +513,9 @@ __global__ __launch_bounds__(BT) void rollout_block_kernel(const KParams* __rest
     const int i = tid / TE, q = tid - (tid / TE) * TE;
     int cnt = 0, neng = 0;
     double mn = INFINITY;
-    const bool act = i < N && !S.dpost[i];   // departed is always True in the training scenario
+    // `agent.departed and not agent.done` (environment.py:1008); departed is always True in the
+    // training scenario
+    const bool act = i < N && !S.dpost[i] && (!S.dep1 || S.dep1[i]);
     if (act) {
       const uint64_t* m = S.emask + i * MW;
       const bool mi = mbit(m, i);

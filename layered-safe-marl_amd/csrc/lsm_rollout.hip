@@ -253,8 +253,9 @@ struct Lds {
   double* trig1;     // [4][N] cos, sin, vx, vy of the post state (node features)
 };
 
-// doubles per env of StateDev::dep
-__host__ __device__ inline int depw(int N) { return 3 * N + 1; }
+// doubles per env of StateDev::dep: departed, timer, init_theta [N], then the accumulated
+// disconnect mask of the step's last ego (the next update_graph's), up to 4 words (E <= 256)
+__host__ __device__ inline int depw(int N) { return 3 * N + 4; }
 
 // LDS bytes of the departure arrays (appended after lds_plan's block)
 __host__ __device__ inline size_t dep_lds_bytes(int N) {
@@ -1876,13 +1877,14 @@ __device__ __forceinline__ void reset_core(const KParams& P, Lds& S, int env, co
   esync<LPE>();   // MT words read out of U1 before compute_dist overwrites it
   if (S.dep0 || keep_done) {
     // departures: undeparted agents are disconnected from the reset's graph observation too;
-    // kept-done agents are disconnected as done
+    // kept-done agents are disconnected as done (the workgroup kernel builds its multi-word
+    // masks itself, reset_block)
     for (int k = lane; k < N; k += LPE) {
       if (S.dep0) {
         S.pth[k] = S.ps[2 * N + k];
         S.psp[k] = S.ps[3 * N + k];
       }
-      S.emask[k] = ego_mask(S, N, L, k);
+      if (LPE != BT) S.emask[k] = ego_mask(S, N, L, k);
     }
     esync<LPE>();
   }
@@ -1928,7 +1930,10 @@ __device__ __forceinline__ void store_state(const KParams& P, Lds& S, const unsi
   if (DYN == 1 && S.dep0) {
     // departures: the post-update heading / speed become the state; departure arrays persist
     GAS double* dg = gptr(P.s.dep) + (size_t)env * depw(N);
-    if (lane == 0) *(GAS uint64_t*)(dg + 3 * N) = S.emask[N - 1];   // next step's update_graph mask
+    // next step's update_graph mask: ego N - 1's words (one word per ego in the one-wave kernels,
+    // ceil(E / 64) in the workgroup kernel)
+    const int MW = LPE == BT ? (E + 63) >> 6 : 1;
+    for (int w = lane; w < MW; w += LPE) ((GAS uint64_t*)(dg + 3 * N))[w] = S.emask[(N - 1) * MW + w];
     for (int j = lane; j < N; j += LPE) {
       S.ps[2 * N + j] = S.pth[j];
       S.ps[3 * N + j] = S.psp[j];
@@ -2475,6 +2480,13 @@ __global__ __launch_bounds__(64, DYN == 0 ? (LPE == 64 ? 4 : 2) : LSM_WAVES_PER_
   // ---- 4. integrate ----------------------------------------------------------------------
   if (lane < N && !inactive_pre(S, lane)) integrate_agent<DYN>(P, S, N, lane);
   __syncthreads();
+  if (DYN == 1 && it + 1 < P.nis) {   // the next inner filter's ego frame: the new headings
+    if (lane < N) {
+      S.ecs[lane] = cos(S.ps[2 * N + lane]);
+      S.ecs[N + lane] = sin(S.ps[2 * N + lane]);
+    }
+    __syncthreads();
+  }
   }
   STAMP(5);
 
@@ -2810,7 +2822,6 @@ int lsm_create(const lsm_config* cfg, lsm_env** out) {
   if (cfg->scenario != LSM_SCENARIO_TRAIN) {
     if (cfg->auto_reset)
       return fail(e, "layout scenarios are evaluation paths (GraphDummyVecEnv, scripts/eval_mpe.py): auto_reset must be 0");
-    if (N > MAXN || N * (1 + L) > MAXE) return fail(e, "layout scenarios need N <= 32 and N * (1 + L) <= 64");
     if (cfg->rng != LSM_RNG_MT19937) return fail(e, "layout scenarios draw on the host: rng must be LSM_RNG_MT19937");
   }
   if (cfg->scenario == LSM_SCENARIO_DEPARTURES && cfg->dynamics != LSM_AIRTAXI)

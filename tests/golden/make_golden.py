@@ -66,7 +66,7 @@ def _dep_rows(world):
 
 def run_case(name, args, seed, ep, steps, value_stored=None, ttr_stored=None, inject=None,
              action_seed=0, runner_episodes=False, sep_curriculum=False, eval_type=None, image_size=None,
-             dummy=False):
+             dummy=False, full_every=50):
     """runner_episodes: step t passes the runner's episode counter ep + t // episode_length, as
     GMPERunner.run does (graph_mpe_runner.py:72-103), so the worker's auto-resets
     (env_wrappers.py:866-871) move through the curriculum. sep_curriculum: the reference's
@@ -161,7 +161,7 @@ def run_case(name, args, seed, ep, steps, value_stored=None, ttr_stored=None, in
         rec["hj_sep"].append(float(hj.separation_distance) if hj is not None else np.nan)
         rec["departed"].append(np.array([a.departed for a in world.agents]))
         changed = t > 0 and not np.array_equal(rec["done"][-1], rec["done"][-2])
-        if t in FULL_STEPS or t % 50 == 0 or changed:
+        if t in FULL_STEPS or t % full_every == 0 or changed:
             full["t%03d_node" % t] = np.array(node, dtype=np.float32)
             full["t%03d_adj" % t] = np.array(adj, dtype=np.float32)
             full["t%03d_edges" % t] = edges
@@ -356,6 +356,16 @@ def main(only=None):
         return
     if only == "ba_merge_l3":
         merge_l3()
+        return
+    # the reference's own Bay Area intersection run (eval_airtaxi.sh:18-31): 16 agents, 6
+    # landmarks each (E = 112: the workgroup kernel), episode_length 750, departure timers
+    cross16 = lambda: run_case("ba_cross_n16", A(scenario_name="navigation_graph_safe_bayarea_cross", num_agents=16,
+                                                 num_landmarks=0, num_env_steps=750 * 4, dynamics_type="airtaxi",
+                                                 episode_length=750, use_safety_filter=True),
+                               seed=0, ep=4, steps=750, value_stored=at_small, ttr_stored=ttr_small, action_seed=20,
+                               image_size=(3300, 3000), dummy=True, full_every=250)
+    if only == "ba_cross16":
+        cross16()
         return
     # World.step's inner loop (core.py:607-631) run num_internal_step times per env step
     nis = [

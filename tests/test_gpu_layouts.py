@@ -18,6 +18,11 @@ from golden_replay import EPKEYS, INFOKEYS, adj_bits, layout_fixture_names, layo
 pytestmark = pytest.mark.gpu
 
 STATE_ATOL = 1e-9
+# airtaxi integrates in closed form on the device (the reference's RK45 right-hand side calls
+# numpy's SIMD sin / cos): ~1e-12 per step, which the 750-step Bay Area intersection grows to
+# ~1e-9 by step 500; its float64 states and distances are compared at 1e-7 there (the north-star
+# bar is 1e-5 on fp32 positions); dones, reached goals, departures and adjacency stay exact
+STATE_ATOL_LONG_AT = 1e-7
 F32_ATOL = 1e-5
 
 
@@ -36,11 +41,19 @@ def _gpu_layout_env(meta, n_envs=1, seed=None):
                           auto_reset=False, emit_edges=True)
 
 
+@pytest.mark.parametrize("kernel", ["auto", "block"])
 @pytest.mark.parametrize("name", layout_fixture_names())
-def test_gpu_layout_matches_reference(name):
+def test_gpu_layout_matches_reference(name, kernel, monkeypatch):
+    """Every layout fixture through the default dispatch (the one-wave generic kernel for
+    E <= 64; the workgroup kernel for the Bay Area intersection at 16 agents, E = 112) and through
+    the workgroup kernel forced (LSM_KERNEL=block)."""
+    if kernel == "block":
+        monkeypatch.setenv("LSM_KERNEL", "block")
     z, meta = load(name)
     env = _gpu_layout_env(meta)
-    assert env.kernel_name.startswith("rollout_kernel<")
+    N = meta["num_agents"]
+    big = N * (1 + env.layout.L) > 64
+    assert env.kernel_name.startswith("rollout_block_kernel<" if (big or kernel == "block") else "rollout_kernel<")
     obs, aid, node, adj, ep = env.reset(meta["ep"])
     np.testing.assert_allclose(obs[0], z["reset0_obs"], rtol=0, atol=F32_ATOL)
     np.testing.assert_allclose(node[0], z["reset0_node"], rtol=0, atol=F32_ATOL)
@@ -50,6 +63,7 @@ def test_gpu_layout_matches_reference(name):
     # every recorded episode, circular_config's second one included (its done agents stay done,
     # unintegrated, with the layout's state: navigation_graph_safe_eval.py:100-121)
     steps = meta["steps"]
+    satol = STATE_ATOL_LONG_AT if (meta["dynamics_type"] == "airtaxi" and steps > 400) else STATE_ATOL
     n_reset = 1
     c_rg, c_mr = _info_col("reached_goal"), _info_col("min_relative_distance")
     c_sf, c_dec = _info_col("Safety filtered"), _info_col("deconflicting_agent_index")
@@ -60,17 +74,17 @@ def test_gpu_layout_matches_reference(name):
         np.testing.assert_array_equal(dones[0], z["dones"][t], err_msg=ctx)
         np.testing.assert_allclose(rew[0], z["rew"][t], rtol=1e-6, atol=1e-5, err_msg=ctx)
         np.testing.assert_array_equal(info[:, c_rg], z["reached"][t], err_msg=ctx)
-        np.testing.assert_allclose(info[:, c_mr], z["minrel"][t], rtol=0, atol=STATE_ATOL, err_msg=ctx)
+        np.testing.assert_allclose(info[:, c_mr], z["minrel"][t], rtol=0, atol=satol, err_msg=ctx)
         np.testing.assert_array_equal(info[:, c_sf].astype(bool), z["sfilt"][t], err_msg=ctx)
         np.testing.assert_array_equal(info[:, c_dec].astype(int), z["decon"][t], err_msg=ctx)
         dep = np.array([d["Departed"] for d in infos[0][:meta["num_agents"]]])
         np.testing.assert_array_equal(dep, z["departed"][t], err_msg=ctx)
         for j, k in enumerate(INFOKEYS):
             # individual_reward is the reward (airtaxi TTR term: float32 interpolation, 1 ulp)
-            tol = dict(rtol=1e-6, atol=1e-5) if k == "individual_reward" else dict(rtol=1e-9, atol=1e-9)
+            tol = dict(rtol=1e-6, atol=1e-5) if k == "individual_reward" else dict(rtol=satol, atol=satol)
             np.testing.assert_allclose(info[:, _info_col(k)], z["info_num"][t][:, j], err_msg=ctx + " info " + k,
                                        **tol)
-        np.testing.assert_allclose(env.state().cpu().numpy()[0], z["state"][t], rtol=0, atol=STATE_ATOL,
+        np.testing.assert_allclose(env.state().cpu().numpy()[0], z["state"][t], rtol=0, atol=satol,
                                    err_msg=ctx)
         np.testing.assert_allclose(obs[0], z["obs"][t], rtol=0, atol=F32_ATOL, err_msg=ctx)
         np.testing.assert_array_equal(adj_bits(adj[0]), z["adj_bits"][t], err_msg=ctx)
@@ -94,21 +108,22 @@ def test_gpu_layout_matches_reference(name):
     env.close()
 
 
-@pytest.mark.parametrize("name", ["ba_merge_n8", "ba_cross_n4", "ev_di_lrmland_n4"])
+@pytest.mark.parametrize("name", ["ba_merge_n8", "ba_cross_n4", "ev_di_lrmland_n4", "ba_cross_n16"])
 def test_gpu_layout_multi_env_matches_oracle(name):
     """5 envs (seeds seed + 1000 k: their own layouts, timers and departures) with random actions
-    against the oracle over one episode and a second reset."""
+    against the oracle over one episode (up to 160 steps) and a second reset; the 16-agent
+    intersection (workgroup kernel) with 3 envs over 130 steps (its first departures)."""
     from oracle.lsm_oracle import OracleEnv
     z, meta = load(name)
     lay, m = layout_for(meta)
-    n, seed = 5, 101
+    n, seed = (3 if name == "ba_cross_n16" else 5), 101
     env = _gpu_layout_env(meta, n_envs=n, seed=seed)
     vt, tt = tables_for(meta)
     oras = [OracleEnv(m, seed + 1000 * k, table_dict(vt), table_dict(tt), integrator="restated")
             for k in range(n)]
     rngs = [np.random.RandomState(seed + 1000 * k) for k in range(n)]
     ep = meta["ep"]
-    steps = min(meta["episode_length"], 160)
+    steps = min(meta["episode_length"], 130 if name == "ba_cross_n16" else 160)
     for rep in range(2):
         g = env.reset(ep)
         for k in range(n):
