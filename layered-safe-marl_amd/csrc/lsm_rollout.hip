@@ -594,34 +594,46 @@ struct WaveRng {
 // ----------------------------------------------------------------------------------
 // HJ grid interpolation (float32; semantics of oracle/hj_grid.py)
 // ----------------------------------------------------------------------------------
+// Every dimension is computed without an early exit and the decision taken once at the end:
+// the table's per-dimension constants then load together instead of one scalar round trip per
+// dimension behind each exit (the latency-bound agent wave runs this in the filter).
 template <int ND>
 __device__ __forceinline__ bool grid_cell(const TableDev& T, const double* s, int& cell, float* w) {
-  float wl[ND], wh[ND];
-  int il[ND];
+  float lo[ND], sp[ND];
+  int nn[ND], per[ND], cs[ND];
 #pragma unroll
   for (int d = 0; d < ND; ++d) {
-    float sd = (float)s[d];
-    float p = (sd - T.lo[d]) / T.sp[d];
-    if (!(p == p) || fabsf(p) > 1.0e9f) return false;
-    const int n = T.n[d];
-    float fl = floorf(p);
+    lo[d] = T.lo[d]; sp[d] = T.sp[d]; nn[d] = T.n[d]; per[d] = T.periodic[d]; cs[d] = T.cstride[d];
+  }
+  float wl[ND], wh[ND];
+  int il[ND];
+  bool ok = true;
+#pragma unroll
+  for (int d = 0; d < ND; ++d) {
+    const float sd = (float)s[d];
+    float p = (sd - lo[d]) / sp[d];
+    ok = ok && (p == p) && !(fabsf(p) > 1.0e9f);   // NaN / runaway coordinate: outside
+    if (!ok) p = 0.0f;                              // keeps the index math finite (result unused)
+    const int n = nn[d];
+    const float fl = floorf(p);
     int f = (int)fl;
-    if (T.periodic[d]) {
+    if (per[d]) {
       wh[d] = p - (float)f;
       int a = f % n;
       if (a < 0) a += n;
       il[d] = a;
     } else {
-      if (p < 0.0f || p > (float)(n - 1)) return false;
+      ok = ok && !(p < 0.0f || p > (float)(n - 1));
       if (f > n - 2) f = n - 2;
       wh[d] = p - (float)f;
       il[d] = f;
     }
     wl[d] = 1.0f - wh[d];
   }
+  if (!ok) return false;
   int c0 = 0;
 #pragma unroll
-  for (int d = 0; d < ND; ++d) c0 += il[d] * T.cstride[d];
+  for (int d = 0; d < ND; ++d) c0 += il[d] * cs[d];
   cell = c0;
 #pragma unroll
   for (int c = 0; c < (1 << ND); ++c) {
@@ -1021,17 +1033,50 @@ __device__ __forceinline__ void filter_ego(const KParams& P, Lds& S, int i, uint
   int jd = -1, jv = -1;
   double dmin = 0.0;
   float vmin = 0.0f;
-  for (int j = 0; j < N; ++j) {
-    if (j == i || inactive_pre(S, j)) continue;
-    const double d = S.dpair[j * N + i];   // pair matrices are [other][ego]: the lanes of an
-    const float v = (float)S.vpair[j * N + i];    // agent wave read consecutive words
-    if (jd < 0 || d < dmin) { jd = j; dmin = d; }
-    if (jv < 0 || v < vmin) { jv = j; vmin = v; }
+  bool in_jv = false;
+  if (NT > 0) {
+    // compile-time N: every pair word of this ego read up front (one LDS round trip for all),
+    // then a branch-free argmin -- first occurrence on ties, np.argmin's rule
+    constexpr int M = NT > 0 ? NT : 1;
+    double dv[M];
+    float vv[M];
+    bool ac[M], in[M];
+#pragma unroll
+    for (int j = 0; j < M; ++j) {
+      ac[j] = S.dpre[j] == 0;
+      dv[j] = S.dpair[j * N + i];   // pair matrices are [other][ego]: the lanes of an agent
+      vv[j] = (float)S.vpair[j * N + i];   // wave read consecutive words
+      in[j] = S.inr[j * N + i] != 0;
+    }
+    if (S.dep0) {   // RealisticScenario layouts only (uniform): not yet departed = inactive
+#pragma unroll
+      for (int j = 0; j < M; ++j) ac[j] = ac[j] && S.dep0[j] != 0;
+    }
+#pragma unroll
+    for (int j = 0; j < M; ++j) {   // selects, no per-pair branches
+      const bool a = ac[j] && j != i;
+      const bool bd = a && (jd < 0 || dv[j] < dmin);
+      const bool bv = a && (jv < 0 || vv[j] < vmin);
+      jd = bd ? j : jd;
+      dmin = bd ? dv[j] : dmin;
+      jv = bv ? j : jv;
+      vmin = bv ? vv[j] : vmin;
+      in_jv = bv ? in[j] : in_jv;
+    }
+  } else {
+    for (int j = 0; j < N; ++j) {
+      if (j == i || inactive_pre(S, j)) continue;
+      const double d = S.dpair[j * N + i];
+      const float v = (float)S.vpair[j * N + i];
+      if (jd < 0 || d < dmin) { jd = j; dmin = d; }
+      if (jv < 0 || v < vmin) { jv = j; vmin = v; }
+    }
+    if (jv >= 0) in_jv = S.inr[jv * N + i] != 0;
   }
   if (jd < 0) return;  // no other active agent
   dec = jv;
   if (dmin > P.coord_range) return;
-  if (!S.inr[jv * N + i]) return;
+  if (!in_jv) return;
   filter_apply<DYN, NT>(P, S, i, jv, vmin, filtered, u0, u1);
 }
 
@@ -2008,6 +2053,121 @@ __device__ __forceinline__ void integrate_agent(const KParams& P, Lds& S, int N,
   }
   S.ps[i] = x; S.ps[N + i] = y; S.ps[2 * N + i] = s2; S.ps[3 * N + i] = s3;
   S.pdist[i] += spd * dt;
+}
+
+// ---- the double integrator's RK45 on a lane pair -------------------------------------------
+// The team kernel's agent wave holds G * N = 32 agents on lanes 0..31 of 64. For the integration
+// lane l runs agent l's x axis and lane l + 32 its y axis: per lane half the divisions and dot
+// products of rk45_di, with the four-component norms (and the speed clamp) formed from both
+// halves through one v_permlane32_swap per 32-bit word. The arithmetic per component and the
+// order of the norm's fma chain (x pos, y pos, x vel, y vel) are rk45_di's, so the result is the
+// same bits (tests/test_gpu_parity.py through the team kernel variants).
+__device__ __forceinline__ double lane32_partner(double v) {
+  const unsigned lo = __double2loint(v), hi = __double2hiint(v);
+  const auto a = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+  const auto b = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+  const bool up = (threadIdx.x & 63) >= 32;
+  return __hiloint2double(up ? b[0] : b[1], up ? a[0] : a[1]);
+}
+
+// (x0, x1, x2, x3) = (x pos, y pos, x vel, y vel) of the pair's components -> rk_norm4
+__device__ __forceinline__ double rk_norm4_pair(double mp, double mv, bool up) {
+  const double qp = lane32_partner(mp), qv = lane32_partner(mv);
+  const double x0 = up ? qp : mp, x1 = up ? mp : qp, x2 = up ? qv : mv, x3 = up ? mv : qv;
+  double s = x0 * x0;
+  s = fma(x1, x1, s);
+  s = fma(x2, x2, s);
+  s = fma(x3, x3, s);
+  return sqrt(s) / 2.0;
+}
+
+// rk45_di for one axis (position p, velocity v, acceleration a) of a lane pair; `up` = y axis.
+// Both lanes of a pair reach the same scalar decisions (same norms), so they stay in step.
+__device__ __forceinline__ void rk45_di_pair(double& p, double& v, double a, double tb, bool up) {
+  const double rtol = 1e-3, atol = 1e-6;
+  const Rk45Tab& T = rk45_tab();
+  double dv[6];
+#pragma unroll
+  for (int s = 1; s < 6; ++s) dv[s] = rk_gemv_const(a, T.A[s], s);
+  const double gb = rk_gemv_const(a, T.B, 6), ge = rk_gemv_const(a, T.E, 7);
+  const double scp = atol + fabs(p) * rtol, scv = atol + fabs(v) * rtol;
+  const double d0 = rk_norm4_pair(p / scp, v / scv, up);
+  const double d1 = rk_norm4_pair(v / scp, a / scv, up);
+  double h0 = (d0 < 1e-5 || d1 < 1e-5) ? 1e-6 : 0.01 * d0 / d1;
+  h0 = (tb < h0) ? tb : h0;
+  const double d2 = rk_norm4_pair(((v + h0 * a) - v) / scp, (a - a) / scv, up) / h0;
+  double h1;
+  if (d1 <= 1e-15 && d2 <= 1e-15) {
+    h1 = (h0 * 1e-3 > 1e-6) ? h0 * 1e-3 : 1e-6;
+  } else {
+    h1 = glibc_pow(0.01 / ((d2 > d1) ? d2 : d1), 1.0 / 5.0);
+  }
+  double h_abs = 100 * h0;
+  if (h1 < h_abs) h_abs = h1;
+  if (tb < h_abs) h_abs = tb;
+  double t = 0.0;
+  double v0 = v;   // K[0] of the step: the step's starting velocity
+  while (t < tb) {
+    bool rejected = false;
+    for (;;) {
+      double t_new = t + h_abs;
+      if (t_new - tb > 0) t_new = tb;
+      const double h = t_new - t;
+      h_abs = fabs(h);
+      double k[7];
+      k[0] = v0;
+#pragma unroll
+      for (int s = 1; s < 6; ++s) k[s] = v + dv[s] * h;
+      const double ynp = p + h * rk_gemv_col(k, T.B, 6);
+      const double ynv = v + h * gb;
+      k[6] = ynv;
+      const double ep = rk_gemv_col(k, T.E, 7), ev = ge;
+      const double ap = fabs(p), anp = fabs(ynp), av = fabs(v), anv = fabs(ynv);
+      const double rp = (ep * h) / (atol + ((ap >= anp) ? ap : anp) * rtol);
+      const double rv = (ev * h) / (atol + ((av >= anv) ? av : anv) * rtol);
+      const double en = rk_norm4_pair(rp, rv, up);
+      if (en < 1) {
+        if (t_new < tb) {
+          double fac = 10.0;
+          if (en > 1e-6) {
+            const double q = 0.9 * glibc_pow(en, -1.0 / 5.0);
+            if (q < fac) fac = q;
+          }
+          if (rejected && fac > 1) fac = 1;
+          h_abs *= fac;
+        }
+        t = t_new;
+        p = ynp;
+        v = ynv;
+        v0 = ynv;
+        break;
+      }
+      const double q = 0.9 * glibc_pow(en, -1.0 / 5.0);
+      h_abs *= (q > 0.2) ? q : 0.2;
+      rejected = true;
+    }
+  }
+}
+
+// integrate_agent<0> on a lane pair (axis `up` of agent i): RK45, speed clamp, travel distance
+__device__ __forceinline__ void integrate_agent_di_pair(const KParams& P, Lds& S, int N, int i, bool up) {
+  const int c = up ? 1 : 0;
+  double p = S.ps[c * N + i], v = S.ps[(2 + c) * N + i];
+  const double a = S.safe[c * N + i];
+  rk45_di_pair(p, v, a, P.dt, up);
+  double q = lane32_partner(v);
+  double sx = up ? q : v, sy = up ? v : q;
+  double spd = sqrt(sx * sx + sy * sy);
+  if (spd > P.max_speed) {
+    v = P.max_speed * v / spd;
+    q = lane32_partner(v);
+    sx = up ? q : v;
+    sy = up ? v : q;
+  }
+  spd = sqrt(sx * sx + sy * sy);
+  S.ps[c * N + i] = p;
+  S.ps[(2 + c) * N + i] = v;
+  if (!up) S.pdist[i] += spd * P.dt;
 }
 
 // numpy's logaddexp(0, z) (npy_logaddexp: x + log1p(exp(y - x)) around the larger argument)

@@ -37,8 +37,9 @@ __host__ __device__ inline size_t team_env_bytes(size_t bytes, int N) {
 // Team kernels target 4 waves / SIMD for the double integrator (<= 128 VGPRs, as rollout_kernel)
 // and 2 for airtaxi.
 // Diagnostic builds (-DLSM_STAMPS, lsm.diag_stamps --team): s_memtime of each env's wave at the
-// phase boundaries: 0 start, 6/7/8 own work of phases A / C / D done, 1-4 after barriers 1-4,
-// 5 end; 13/14 realtime start / end; 15 HW_ID | XCC_ID << 32. Never in the product library.
+// phase boundaries: 0 start, 12 record in LDS, 6/7/8 own work of phases A / C / D done, 1-4 after
+// barriers 1-4, 5 end; 9 / 10 / 11 inside the agent phases B / D; 13/14 realtime start / end;
+// 15 HW_ID | XCC_ID << 32. Never in the product library.
 #ifdef LSM_STAMPS
 #define TSTAMP(k)                                                                                  \
   do {                                                                                             \
@@ -103,6 +104,7 @@ void rollout_team_kernel(const KParams* __restrict__ Pp, const KStep K) {
     }
     rec_copy<LPE>((const GAS f32x4*)gptr(P.s.rec) + (size_t)env * P.s.rec_stride16, (f32x4*)lbase, P.s.rec16);
     esync<LPE>();
+    TSTAMP(12);
     if (lane < N) {
       S.dpre[lane] = S.dpost[lane];
       S.rpre[lane] = S.rpost[lane];
@@ -168,7 +170,18 @@ void rollout_team_kernel(const KParams* __restrict__ Pp, const KStep K) {
     if (alane) filter_agent<DYN, NT>(P, A, N, ai, A.cur[C_FILT] != 0.0);
     esync<LPE>();   // every filter of the env has read the pre-step state
     TSTAMP(9);
-    if (alane && !A.dpre[ai]) integrate_agent<DYN>(P, A, N, ai);
+    if (DYN == 0 && G * NT <= 32) {
+      // the double integrator's RK45 on lane pairs: lane l the x axis of agent l, lane l + 32
+      // its y axis (integrate_agent_di_pair); both lanes of a pair have the same activity
+      const int hl = lane & 31;
+      const int g2 = hl / NT, i2 = hl - g2 * NT;
+      if (g2 < G && env0 + g2 < P.n_envs) {
+        Lds A2 = carve(smem + (size_t)g2 * B, N, NL, E, F, false);
+        if (!A2.dpre[i2]) integrate_agent_di_pair(P, A2, N, i2, lane >= 32);
+      }
+    } else if (alane && !A.dpre[ai]) {
+      integrate_agent<DYN>(P, A, N, ai);
+    }
   }
   __syncthreads();
   TSTAMP(2);

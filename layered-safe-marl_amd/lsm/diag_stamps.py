@@ -24,7 +24,8 @@ def build_stamps():
     from . import build
     cmd = [build.HIPCC] + build.FLAGS + ["-shared", "-DLSM_STAMPS", "-o", STAMP_LIB, build.SRC,
                                         os.path.join(CSRC, "lsm_edges.hip"),
-                                        os.path.join(CSRC, "lsm_buffer.hip")]
+                                        os.path.join(CSRC, "lsm_buffer.hip"),
+                                        os.path.join(CSRC, "lsm_metrics.hip")]
     subprocess.check_call(cmd, cwd=CSRC)
 
 
@@ -69,7 +70,7 @@ def main():
         if t >= 10:
             s = stamps.cpu().numpy().astype(np.float64)
             tstamps.append(s[:, :9].copy())
-            tstamps12.append(s[:, :12].copy())
+            tstamps12.append(s[:, :13].copy())
             stamps.zero_()
             acc.append(np.diff(s[:, [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10]], axis=1))
             t0 = s[:, 13].min()
@@ -87,7 +88,8 @@ def main():
                                                       np.percentile(v, 90)))
         print("%-18s %12.0f" % ("total", tot))
         ag = np.concatenate(tstamps12, axis=0)
-        for name, i, j in [("B filter", 1, 9), ("B integrate", 9, 2), ("D reward", 3, 10),
+        for name, i, j in [("A record", 0, 12), ("A decode+pairs", 12, 6), ("B filter", 1, 9),
+                           ("B integrate", 9, 2), ("D reward", 3, 10),
                            ("D info", 10, 11), ("D rows+stats", 11, 8)]:
             v = ag[:, j] - ag[:, i]
             v = v[(ag[:, i] != 0) & (ag[:, j] != 0)]
