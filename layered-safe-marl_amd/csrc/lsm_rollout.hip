@@ -224,6 +224,7 @@ struct Lds {
   double* aa;        // [N][N] float64 agent-agent distances (episode stats)
   double* aa2;       // [N][N] np.linalg.norm agent-agent distances (min relative distance, collisions)
   uint32_t* mt;      // [MT_WORDS]
+  uint32_t* mtn;     // [MT_N] the next MT19937 block (team kernel resets; U1 after scratch, or U2)
   double* scen;      // [SCEN_WS]
   double* scratch;   // [2][MAXN]
   // U2
@@ -401,7 +402,8 @@ __host__ __device__ inline LdsPlan lds_plan(int N, int NL, int E, int F, bool bl
   size_t u1sz = b > e ? b : e;
   const size_t h0 = align16(4 * WAVE * F);   // node staging for up to 64 pairs
   u1sz = u1sz > h0 ? u1sz : h0;
-  size_t f1 = align16(8 * N * N), f2 = f1 + align16(8 * N * N), f3 = f2 + align16(N * N);
+  // pair matrices dpair, vpair, inr, then the team kernel's per-ego filter slots (filter_slot)
+  size_t f1 = align16(8 * N * N), f2 = f1 + align16(8 * N * N), f3 = f2 + align16(N * N) + align16(32 * N);
   if (lean) u1sz = u1sz > f3 ? u1sz : f3;   // the pair matrices at the head of U1
   o = u1 + u1sz;
   // U2
@@ -415,6 +417,13 @@ __host__ __device__ inline LdsPlan lds_plan(int N, int NL, int E, int F, bool bl
   size_t m = lean ? g2 : (f3 > g2 ? f3 : g2);
   if (F == 10) m = m > (size_t)(8 * 2 * 64) ? m : (size_t)(8 * 2 * 64);   // magnetic partials (DI, filter off)
   m = m > (size_t)(8 * LSM_INFO_FIELDS * N) ? m : (size_t)(8 * LSM_INFO_FIELDS * N);   // info rows
+  // the next MT19937 block of a team-kernel reset (live with mt / scen; U2 is free then): after
+  // U1's scratch when it fits, else at the U2 base (the team kernels' layouts have room either way,
+  // lsm_create checks)
+  const size_t mtb = align16(4 * MT_N);
+  const bool mtn_u1 = u1sz - e >= mtb;
+  p.off[k++] = mtn_u1 ? u1 + e : u2;
+  if (!mtn_u1 && m < mtb) m = mtb;
   o = u2 + m;
   p.bytes = o;
   return p;
@@ -461,6 +470,7 @@ __device__ __forceinline__ Lds carve(unsigned char* base, int N, int NL, int E, 
   L.feat = (double*)(base + p.off[k++]);
   L.egooff = (double*)(base + p.off[k++]);
   L.stage = (float*)(base + p.off[k++]);
+  L.mtn = (uint32_t*)(base + p.off[k++]);
   L.info = L.feat;   // U2 base (= dpair outside the lean layout)
   L.lean = lean;
   L.ex = L.ey = nullptr;
@@ -525,6 +535,7 @@ __device__ __forceinline__ Lds carve_block(unsigned char* base, int N, int NL, i
   L.dpair = (double*)(base + p.off[k++]);
   L.stage = (float*)(base + p.off[k++]);
   L.fval = nullptr; L.aa = nullptr; L.aa2 = nullptr; L.vpair = nullptr; L.inr = nullptr;
+  L.mtn = nullptr;
   L.info = L.dpair;
   L.lean = false;
   L.dep0 = L.dep1 = L.tmr = nullptr;
@@ -1022,14 +1033,14 @@ template <int DYN, int NT>
 __device__ __forceinline__ void filter_apply(const KParams& P, const Lds& S, int i, int jv, float vmin,
                                              uint8_t& filtered, double& u0, double& u1);
 
+// The deconflicting choice of ego i from its pair words (safety_filter.py:395-423): jv = argmin of
+// the HJ value over the other active agents (dec), and whether the filter then applies (the
+// nearest agent within the coordination range, the value lookup in range). Returns false when
+// there is no other active agent.
 template <int DYN, int NT>
-__device__ __forceinline__ void filter_ego(const KParams& P, Lds& S, int i, uint8_t& filtered, int& dec,
-                                  double& u0, double& u1) {
+__device__ __forceinline__ bool filter_select(const KParams& P, const Lds& S, int i, int& jv_out, float& vmin_out,
+                                              bool& apply) {
   LSM_DIMS;
-  u0 = S.raw[i];
-  u1 = S.raw[N + i];
-  filtered = 0;
-  dec = -1;
   int jd = -1, jv = -1;
   double dmin = 0.0;
   float vmin = 0.0f;
@@ -1073,11 +1084,91 @@ __device__ __forceinline__ void filter_ego(const KParams& P, Lds& S, int i, uint
     }
     if (jv >= 0) in_jv = S.inr[jv * N + i] != 0;
   }
-  if (jd < 0) return;  // no other active agent
+  jv_out = jv;
+  vmin_out = vmin;
+  apply = jd >= 0 && !(dmin > P.coord_range) && in_jv;
+  (void)E; (void)F;
+  return jd >= 0;
+}
+
+template <int DYN, int NT>
+__device__ __forceinline__ void filter_ego(const KParams& P, Lds& S, int i, uint8_t& filtered, int& dec,
+                                  double& u0, double& u1) {
+  LSM_DIMS;
+  u0 = S.raw[i];
+  u1 = S.raw[N + i];
+  filtered = 0;
+  dec = -1;
+  int jv;
+  float vmin;
+  bool apply;
+  if (!filter_select<DYN, NT>(P, S, i, jv, vmin, apply)) return;   // no other active agent
   dec = jv;
-  if (dmin > P.coord_range) return;
-  if (!in_jv) return;
-  filter_apply<DYN, NT>(P, S, i, jv, vmin, filtered, u0, u1);
+  if (apply) filter_apply<DYN, NT>(P, S, i, jv, vmin, filtered, u0, u1);
+  (void)E; (void)F;
+}
+
+// Team kernel: the filter split over its phases. Phase A (ego i's env wave, whose memory latency
+// the other waves of the SIMD hide) selects the deconflicting agent and interpolates the HJ
+// gradient there; phase B (the latency-bound agent wave) reads the slot and does the QP only.
+// Slot of ego i: 8 words right after the pair matrices (U2, or U1 in the lean layout; free space
+// there until phase D / E -- lds_plan): g[0..4], V, jv, status (0 ego inactive, 1 no other
+// active agent, 2 unfiltered with dec = jv, 3 filter applies).
+__device__ __forceinline__ float* filter_slot(const Lds& S, int N, int i) {
+  return (float*)((uint8_t*)S.inr + align16_((size_t)N * N)) + 8 * i;
+}
+
+template <int DYN, int NT>
+__device__ __forceinline__ void filter_qp(const KParams& P, const Lds& S, int i, int jv, float vmin,
+                                          const double* rel, const float* g, uint8_t& filtered, double& u0,
+                                          double& u1);
+
+template <int DYN, int NT>
+__device__ __forceinline__ void filter_prep(const KParams& P, Lds& S, int i) {
+  LSM_DIMS;
+  float* f = filter_slot(S, N, i);
+  int st = 0, jv = -1;
+  float vmin = 0.0f;
+  float g[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+  if (!inactive_pre(S, i)) {
+    bool apply;
+    if (!filter_select<DYN, NT>(P, S, i, jv, vmin, apply)) {
+      st = 1;
+    } else if (!apply) {
+      st = 2;
+    } else {
+      st = 3;
+      double rel[5];
+      rel_state<DYN>(S, N, i, jv, rel);
+      if (DYN == 0) interp_grad<4>(P.val, rel, g); else interp_grad<5>(P.val, rel, g);
+    }
+  }
+  float4* f4 = (float4*)f;
+  f4[0] = make_float4(g[0], g[1], g[2], g[3]);
+  f4[1] = make_float4(g[4], vmin, __int_as_float(jv), __int_as_float(st));
+}
+
+// Phase B of the team kernel: filter_agent with the slot filter_prep filled.
+template <int DYN, int NT>
+__device__ __forceinline__ void filter_agent_slot(const KParams& P, Lds& S, int N, int i, bool filter_on) {
+  double u0 = S.raw[i], u1 = S.raw[N + i];
+  if (filter_on) {
+    const float4* f4 = (const float4*)filter_slot(S, N, i);
+    const float4 a = f4[0], b = f4[1];
+    const int st = __float_as_int(b.w), jv = __float_as_int(b.z);
+    uint8_t fl = 0;
+    if (st == 3) {
+      double rel[5];
+      rel_state<DYN>(S, N, i, jv, rel);
+      const float g[5] = {a.x, a.y, a.z, a.w, b.x};
+      filter_qp<DYN, NT>(P, S, i, jv, b.y, rel, g, fl, u0, u1);
+    }
+    S.sfilt[i] = fl;
+    S.decon[i] = st >= 2 ? jv : -1;
+  }
+  S.safe[i] = u0;
+  S.safe[N + i] = u1;
+  S.adiff[i] = blas_norm2(S.raw[i] - u0, S.raw[N + i] - u1);
 }
 
 // The filter for ego i once its deconflicting agent jv (argmin of the HJ value, V = vmin in
@@ -1804,10 +1895,12 @@ __device__ __forceinline__ void summary_rolled(const KParams& P, const Lds& S, d
 // Device reset of one env (MultiAgentGraphEnv.reset, environment.py:1046-1074). Expects the
 // env's persistent per-agent arrays in LDS (S.stats, S.rpost = reached_goal before reset).
 // Everything of the reset up to the outputs: summary, curriculum block, scenario draw,
-// per-agent episode arrays.
+// per-agent episode arrays. In three pieces (reset_head, the draw, reset_tail) so the team
+// kernel can run the draws of its envs one lane per env (lsm_team.h).
+
+// Summary of the ending episode, the new curriculum block and the HJ separation shift.
 template <int DYN, int LPE, int NT>
-__device__ __forceinline__ void reset_core(const KParams& P, Lds& S, int env, const double* cur_new,
-                                           const double* layout = nullptr) {
+__device__ __forceinline__ void reset_head(const KParams& P, Lds& S, int env, const double* cur_new) {
   const int lane = threadIdx.x & (LPE - 1);
   LSM_DIMS;
   GAS double* prev = gptr(P.s.prev) + (size_t)env * 8;
@@ -1835,11 +1928,65 @@ __device__ __forceinline__ void reset_core(const KParams& P, Lds& S, int env, co
       S.sep[1] = cur_new[C_SEP];
     }
   }
-  bool keep_done = false;   // scenario_circular_config leaves done agents done (see below)
+  esync<LPE>();
+}
+
+// random_scenario's parameters of an env (its curriculum block in S.cur)
+template <int DYN, int NT>
+__device__ __forceinline__ ScenarioParams scenario_params(const KParams& P, const Lds& S) {
+  LSM_DIMS;
   ScenarioParams sp;
   sp.dyn = DYN; sp.N = N; sp.L = L; sp.world_size = P.world_size; sp.coordination_range = P.coord_range;
   sp.goal_speed_min = P.gs_min; sp.goal_speed_max = P.gs_max;
   sp.ratio_airtaxi = S.cur[C_RAT]; sp.ratio_scenario = S.cur[C_RSC]; sp.two_pi = P.two_pi; sp.pi = P.pi;
+  return sp;
+}
+
+// The new episode's per-agent arrays once the scenario is in S.ps / S.lm.
+template <int DYN, int LPE, int NT>
+__device__ __forceinline__ void reset_tail(const KParams& P, Lds& S, bool keep_done) {
+  const int lane = threadIdx.x & (LPE - 1);
+  LSM_DIMS;
+  for (int k = lane; k < NL; k += LPE) {
+    S.lmsc[k] = sin(S.lm[2 * NL + k]);
+    S.lmsc[NL + k] = cos(S.lm[2 * NL + k]);
+  }
+  for (int k = lane; k < N; k += LPE) {
+    // every layout sets agent.done = False except scenario_circular_config (navigation_graph_safe_
+    // eval.py:100-121): there a done agent stays done, with the layout's state as its frozen state
+    const int32_t d = keep_done ? S.dpost[k] : 0;
+    S.dpre[k] = d; S.dpost[k] = d; S.rpre[k] = 0; S.rpost[k] = 0;
+    S.emask[k] = 0;
+    S.winfo[k] = -1.0; S.winfo[N + k] = -1.0; S.winfo[2 * N + k] = -1.0; S.winfo[3 * N + k] = 0.0;
+    for (int q = 0; q < NSTAT; ++q) S.stats[q * N + k] = (q == 4) ? INFINITY : 0.0;
+    S.pdist[k] = 0.0;
+    S.gmt[k] = plain_norm2(S.ps[k] - S.lm[k], S.ps[N + k] - S.lm[NL + k]) / P.max_speed;
+  }
+  if (lane == 0) { S.step[0] = 0; S.step[1] = 0; }
+  esync<LPE>();   // MT words read out of U1 before compute_dist overwrites it
+  if (S.dep0 || keep_done) {
+    // departures: undeparted agents are disconnected from the reset's graph observation too;
+    // kept-done agents are disconnected as done (the workgroup kernel builds its multi-word
+    // masks itself, reset_block)
+    for (int k = lane; k < N; k += LPE) {
+      if (S.dep0) {
+        S.pth[k] = S.ps[2 * N + k];
+        S.psp[k] = S.ps[3 * N + k];
+      }
+      if (LPE != BT) S.emask[k] = ego_mask(S, N, L, k);
+    }
+    esync<LPE>();
+  }
+}
+
+template <int DYN, int LPE, int NT>
+__device__ __forceinline__ void reset_core(const KParams& P, Lds& S, int env, const double* cur_new,
+                                           const double* layout = nullptr) {
+  const int lane = threadIdx.x & (LPE - 1);
+  LSM_DIMS;
+  reset_head<DYN, LPE, NT>(P, S, env, cur_new);
+  bool keep_done = false;   // scenario_circular_config leaves done agents done (see reset_tail)
+  const ScenarioParams sp = scenario_params<DYN, NT>(P, S);
   if (layout) {
     // lsm_reset_layout: the host's evaluation layout replaces random_scenario (no device draws)
     const int LD = 4 * N + 4 * NL + (S.dep0 ? 3 * N : 0) + 1;   // last word: keep done
@@ -1895,7 +2042,9 @@ __device__ __forceinline__ void reset_core(const KParams& P, Lds& S, int env, co
     rng.key = S.mt;
     rng.pos = (int)S.mt[MT_N];
     // every lane runs the identical draw sequence and stores the identical values
+#ifndef LSM_XP_NOSCEN   // diagnostic bound only (the previous episode's layout is kept)
     random_scenario(rng, sp, S.ps, S.lm, S.scen);
+#endif
     esync<LPE>();
     if (lane == 0) S.mt[MT_N] = (uint32_t)rng.pos;
     esync<LPE>();
@@ -1903,36 +2052,7 @@ __device__ __forceinline__ void reset_core(const KParams& P, Lds& S, int env, co
   GAS uint32_t* mtw = gptr(P.s.mt) + (size_t)env * MT_WORDS;
   for (int k = lane; k < MT_WORDS; k += LPE) mtw[k] = S.mt[k];
   }
-  for (int k = lane; k < NL; k += LPE) {
-    S.lmsc[k] = sin(S.lm[2 * NL + k]);
-    S.lmsc[NL + k] = cos(S.lm[2 * NL + k]);
-  }
-  for (int k = lane; k < N; k += LPE) {
-    // every layout sets agent.done = False except scenario_circular_config (navigation_graph_safe_
-    // eval.py:100-121): there a done agent stays done, with the layout's state as its frozen state
-    const int32_t d = keep_done ? S.dpost[k] : 0;
-    S.dpre[k] = d; S.dpost[k] = d; S.rpre[k] = 0; S.rpost[k] = 0;
-    S.emask[k] = 0;
-    S.winfo[k] = -1.0; S.winfo[N + k] = -1.0; S.winfo[2 * N + k] = -1.0; S.winfo[3 * N + k] = 0.0;
-    for (int q = 0; q < NSTAT; ++q) S.stats[q * N + k] = (q == 4) ? INFINITY : 0.0;
-    S.pdist[k] = 0.0;
-    S.gmt[k] = plain_norm2(S.ps[k] - S.lm[k], S.ps[N + k] - S.lm[NL + k]) / P.max_speed;
-  }
-  if (lane == 0) { S.step[0] = 0; S.step[1] = 0; }
-  esync<LPE>();   // MT words read out of U1 before compute_dist overwrites it
-  if (S.dep0 || keep_done) {
-    // departures: undeparted agents are disconnected from the reset's graph observation too;
-    // kept-done agents are disconnected as done (the workgroup kernel builds its multi-word
-    // masks itself, reset_block)
-    for (int k = lane; k < N; k += LPE) {
-      if (S.dep0) {
-        S.pth[k] = S.ps[2 * N + k];
-        S.psp[k] = S.ps[3 * N + k];
-      }
-      if (LPE != BT) S.emask[k] = ego_mask(S, N, L, k);
-    }
-    esync<LPE>();
-  }
+  reset_tail<DYN, LPE, NT>(P, S, keep_done);
 }
 
 template <int DYN, int LPE, int NT>
@@ -1943,7 +2063,9 @@ __device__ __forceinline__ void reset_env(const KParams& P, Lds& S, int env, con
   reset_core<DYN, LPE, NT>(P, S, env, cur_new, layout);
   compute_dist<LPE, NT>(P, S, nullptr, true);
   if (lane < N) write_obs<DYN, NT>(P, S, env, lane);
+#ifndef LSM_XP_NORESETEMIT   // diagnostic bound only: no graph outputs after a reset
   emit_graph<DYN, LPE, NT>(P, S, env);
+#endif
 }
 
 // Record copy between HBM and the head of the env's LDS block: up to 4 float4 per lane in

@@ -54,6 +54,123 @@ __host__ __device__ inline size_t team_env_bytes(size_t bytes, int N) {
 #define TRTSTAMP(k) do { } while (0)
 #endif
 
+// ---- resets: the scenario draws of the workgroup's envs, one lane per env -----------------
+// random_scenario is a long scalar sequence (rejection loops, atan2, ~120 MT19937 doubles at N =
+// 8) that every lane of an env's wave used to run identically; with all G waves of the 4
+// workgroups of a CU doing so at once, an auto-reset step cost ~2.5 plain steps. Here each env's
+// wave prepares its stream (the rest of the current MT19937 block in LDS plus the next block,
+// generated out of place), then ONE wave runs the draws of every resetting env of the workgroup,
+// lane g for env g, and each env's wave finishes its own reset.
+
+// The next MT19937 block (HostMT::gen's arithmetic) into nxt, leaving key intact. Cooperative over
+// the env's 64 lanes: element i >= 227 reads nxt[i - 227], so chunks of 64 run in order.
+__device__ __forceinline__ void mt_next_block(const uint32_t* key, uint32_t* nxt) {
+  const int lane = threadIdx.x & 63;
+  for (int i = lane; i < MT_N - MT_M; i += 64) nxt[i] = mt_twist1(key[i], key[i + 1], key[i + MT_M]);
+  esync<64>();
+  for (int base = MT_N - MT_M; base < MT_N - 1; base += 64) {
+    const int i = base + lane;
+    if (i < MT_N - 1) nxt[i] = mt_twist1(key[i], key[i + 1], nxt[i - (MT_N - MT_M)]);
+    esync<64>();
+  }
+  if (lane == 0) nxt[MT_N - 1] = mt_twist1(key[MT_N - 1], nxt[0], nxt[MT_M - 1]);
+  esync<64>();
+}
+
+// One env's numpy stream for a lane that draws that env's scenario alone: the current block
+// from pos on, then the next block. A scenario needing more (over 624 words beyond the current
+// block) sets `over`; the env's wave then redraws it with the cooperative stream.
+constexpr uint32_t MT_OVER = 0xffffffffu;
+struct LaneMT {
+  const uint32_t* key;
+  const uint32_t* nxt;
+  int pos;
+  bool over;
+  __device__ __forceinline__ uint32_t next32() {
+    uint32_t y = 0;
+    if (pos < MT_N) y = key[pos];
+    else if (pos < 2 * MT_N) y = nxt[pos - MT_N];
+    else over = true;
+    ++pos;
+    return mt_temper(y);
+  }
+  __device__ __forceinline__ double next_double() {
+    const uint32_t a = next32() >> 5, b = next32() >> 6;
+    return (a * 67108864.0 + b) / 9007199254740992.0;
+  }
+  __device__ __forceinline__ double uniform(double lo, double hi) {
+    const double range = hi - lo;
+    return lo + range * next_double();
+  }
+};
+
+// env wave: summary, curriculum, shift; the MT19937 stream staged in LDS (start pos kept)
+template <int DYN, int NT>
+__device__ __forceinline__ int team_reset_prep(const KParams& P, Lds& S, int env, const double* cur_new) {
+  const int lane = threadIdx.x & 63;
+  reset_head<DYN, 64, NT>(P, S, env, cur_new);
+  if (P.rng == LSM_RNG_PHILOX) return 0;
+  const GAS uint32_t* mtg = gptr(P.s.mt) + (size_t)env * MT_WORDS;
+  for (int k = lane; k < MT_WORDS; k += 64) S.mt[k] = mtg[k];
+  esync<64>();
+  const int p0 = (int)S.mt[MT_N];
+  mt_next_block(S.mt, S.mtn);
+  return p0;
+}
+
+// lane g of one wave: env g's scenario (its LDS block at smem + g * B)
+template <int DYN, int NT>
+__device__ __forceinline__ void team_scenario(const KParams& P, unsigned char* smem, uint32_t B, int g, int env) {
+  LSM_DIMS;
+  Lds S = carve(smem + (size_t)g * B, N, NL, E, F, DYN == 1 && P.lean != 0);
+  const ScenarioParams sp = scenario_params<DYN, NT>(P, S);
+  if (P.rng == LSM_RNG_PHILOX) {
+    GAS uint32_t* rw = gptr(P.s.mt) + (size_t)env * MT_WORDS + MT_N;
+    const uint32_t ridx = *rw - (uint32_t)MT_N;
+    Philox rng;
+    rng.init((uint32_t)(P.seed + 1000 * (P.env_offset + env)), ridx);
+    random_scenario(rng, sp, S.ps, S.lm, S.scen);
+    *rw = ridx + 1 + (uint32_t)MT_N;
+    return;
+  }
+  LaneMT rng;
+  rng.key = S.mt;
+  rng.nxt = S.mtn;
+  rng.pos = (int)S.mt[MT_N];
+  rng.over = false;
+  random_scenario(rng, sp, S.ps, S.lm, S.scen);
+  S.mt[MT_N] = rng.over ? MT_OVER : (uint32_t)rng.pos;
+}
+
+// env wave: the stream's new state to HBM (a redraw if the lane ran out), then reset_tail
+template <int DYN, int NT>
+__device__ __forceinline__ void team_reset_finish(const KParams& P, Lds& S, int env, int p0) {
+  const int lane = threadIdx.x & 63;
+  if (P.rng != LSM_RNG_PHILOX) {
+    GAS uint32_t* mtw = gptr(P.s.mt) + (size_t)env * MT_WORDS;
+    const uint32_t p = S.mt[MT_N];
+    esync<64>();
+    if (p == MT_OVER) {
+      // rare: more draws than the two staged blocks -- the cooperative stream from the start
+      WaveRng<64> rng;
+      rng.key = S.mt;
+      rng.pos = p0;
+      const ScenarioParams sp = scenario_params<DYN, NT>(P, S);
+      random_scenario(rng, sp, S.ps, S.lm, S.scen);
+      esync<64>();
+      if (lane == 0) S.mt[MT_N] = (uint32_t)rng.pos;
+      esync<64>();
+      for (int k = lane; k < MT_WORDS; k += 64) mtw[k] = S.mt[k];
+    } else if (p <= (uint32_t)MT_N) {
+      if (lane == 0) mtw[MT_N] = p;   // the block itself is unchanged
+    } else {
+      for (int k = lane; k < MT_N; k += 64) mtw[k] = S.mtn[k];   // the next block became current
+      if (lane == 0) mtw[MT_N] = p - (uint32_t)MT_N;
+    }
+  }
+  reset_tail<DYN, 64, NT>(P, S, false);
+}
+
 template <int DYN, int NT, int G>
 __global__ __launch_bounds__(64 * G) __attribute__((amdgpu_waves_per_eu(DYN == 0 ? 4 : 2)))
 void rollout_team_kernel(const KParams* __restrict__ Pp, const KStep K) {
@@ -159,6 +276,10 @@ void rollout_team_kernel(const KParams* __restrict__ Pp, const KStep K) {
         S.vpair[p] = ok ? v : INFINITY;
         S.inr[p] = ok ? 1 : 0;
       }
+      // the deconflicting choice and the HJ gradient lookup of every ego, here where the other
+      // waves of the SIMD hide the gather; the agent wave does the QP in B (filter_agent_slot)
+      esync<LPE>();
+      if (lane < N) filter_prep<DYN, NT>(P, S, lane);
     }
   }
   TSTAMP(6);
@@ -167,7 +288,7 @@ void rollout_team_kernel(const KParams* __restrict__ Pp, const KStep K) {
 
   // ---- B. filter + integration, one lane per (env, agent) ------------------------------------
   if (w == WB) {
-    if (alane) filter_agent<DYN, NT>(P, A, N, ai, A.cur[C_FILT] != 0.0);
+    if (alane) filter_agent_slot<DYN, NT>(P, A, N, ai, A.cur[C_FILT] != 0.0);
     esync<LPE>();   // every filter of the env has read the pre-step state
     TSTAMP(9);
     if (DYN == 0 && G * NT <= 32) {
@@ -242,32 +363,51 @@ void rollout_team_kernel(const KParams* __restrict__ Pp, const KStep K) {
   __syncthreads();
   TSTAMP(4);
 
-  // ---- E. info rows, dones, then the auto-reset or what the speculation did not cover ----------
-  if (!live) return;
-  rec_copy<LPE>((const f32x4*)S.info, (GAS f32x4*)(gptr(P.o.info) + (size_t)env * N * LSM_INFO_FIELDS),
-                N * LSM_INFO_FIELDS / 2);
-  bool my_done = true;
-  if (lane < N) {
-    my_done = S.dpost[lane] || cstep >= P.episode_length;
-    gptr(P.o.dones)[(size_t)env * N + lane] = my_done ? 1 : 0;
-  }
-  const bool all_done = __all(my_done);
-  write_masks(P, env, N, lane, my_done, all_done);
-  esync<LPE>();   // info rows read out of U2 before the node rows / a reset overwrite it
-  if (lane == 0) { S.step[0] = cstep; S.step[1] = 0; }
-  if (P.auto_reset && all_done) {
-    if (lane == 0) gptr(P.o.reset_flag)[env] = 1;
-    reset_env<DYN, LPE, NT>(P, S, env, K.cur_new);
-    esync<LPE>();
-    store_state<DYN, LPE, NT>(P, S, lbase, env, true);
-  } else {
-    if (lane == 0) gptr(P.o.reset_flag)[env] = 0;
-    // adjacency already stored in D except WD's (emit_graph rewrites it if a status changed)
+  // ---- E. info rows, dones, then what the speculation did not cover, or the auto-reset --------
+  __shared__ int team_rs[G];   // this step's auto-resets of the workgroup's envs
+  bool rs = false;
+  if (live) {
+    rec_copy<LPE>((const f32x4*)S.info, (GAS f32x4*)(gptr(P.o.info) + (size_t)env * N * LSM_INFO_FIELDS),
+                  N * LSM_INFO_FIELDS / 2);
+    bool my_done = true;
+    if (lane < N) {
+      my_done = S.dpost[lane] || cstep >= P.episode_length;
+      gptr(P.o.dones)[(size_t)env * N + lane] = my_done ? 1 : 0;
+    }
+    const bool all_done = __all(my_done);
+    write_masks(P, env, N, lane, my_done, all_done);
+    esync<LPE>();   // info rows read out of U2 before the node rows / a reset overwrite it
+    if (lane == 0) { S.step[0] = cstep; S.step[1] = 0; }
+    rs = P.auto_reset && all_done;
+    if (lane == 0) gptr(P.o.reset_flag)[env] = rs ? 1 : 0;
+    if (!rs) {
+      // adjacency already stored in D except WD's (emit_graph rewrites it if a status changed)
 #ifndef LSM_XP_NOOUT
-    emit_graph<DYN, LPE, NT>(P, S, env, chunked && w != WD);
+      emit_graph<DYN, LPE, NT>(P, S, env, chunked && w != WD);
 #endif
-    esync<LPE>();
-    store_state<DYN, LPE, NT>(P, S, lbase, env, false);
+      esync<LPE>();
+      store_state<DYN, LPE, NT>(P, S, lbase, env, false);
+    }
+  }
+  if (lane == 0) team_rs[w] = rs ? 1 : 0;
+  __syncthreads();
+  int nrs = 0;
+#pragma unroll
+  for (int g = 0; g < G; ++g) nrs += team_rs[g];
+  if (nrs != 0) {   // workgroup-uniform
+    int p0 = 0;
+    if (rs) p0 = team_reset_prep<DYN, NT>(P, S, env, K.cur_new);
+    __syncthreads();
+    if (w == 0 && lane < G && team_rs[lane]) team_scenario<DYN, NT>(P, smem, B, lane, env0 + lane);
+    __syncthreads();
+    if (rs) {
+      team_reset_finish<DYN, NT>(P, S, env, p0);
+      compute_dist<LPE, NT>(P, S, nullptr, true);
+      if (lane < N) write_obs<DYN, NT>(P, S, env, lane);
+      emit_graph<DYN, LPE, NT>(P, S, env);
+      esync<LPE>();
+      store_state<DYN, LPE, NT>(P, S, lbase, env, true);
+    }
   }
   TSTAMP(5);
   TRTSTAMP(14);

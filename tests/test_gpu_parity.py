@@ -613,3 +613,55 @@ def test_gpu_collision_forces_reported_never_applied(kernel, monkeypatch):
     assert strong >= 2
     on.close()
     off.close()
+
+
+@pytest.mark.parametrize("team", ["4", "2", "8"])
+@pytest.mark.parametrize("dyn,N", [("double_integrator", 8), ("airtaxi", 16)])
+def test_gpu_team_kernel_resets_match_oracle(dyn, N, team, monkeypatch):
+    """The team kernel's auto-resets (all of a workgroup's envs, or some, reset in one launch; the
+    scenario draws run one lane per env from the staged MT19937 stream, crossing block boundaries
+    over successive resets) against the oracle: 10-step episodes, 75 steps (7 resets per env),
+    envs driven all-done early at different steps so resets do not line up, every output."""
+    import torch
+    if dyn == "airtaxi" and team == "8":
+        pytest.skip("8 airtaxi envs of 16 agents do not fit one 64-lane agent wave")
+    monkeypatch.setenv("LSM_TEAM", team)
+    ws = 4 if dyn == "double_integrator" else 6
+    meta = dict(dynamics_type=dyn, num_agents=N, num_landmarks=2, world_size=ws, episode_length=10,
+                num_env_steps=10 * 4, n_rollout_threads=1, use_safety_filter=True, use_masking=True,
+                num_internal_step=1, seed=21, env_seed=21)
+    n_envs = 15   # a partly filled last workgroup
+    env = _gpu_env(meta, n_envs=n_envs, seed=21)
+    assert env.kernel_name.startswith("rollout_team_kernel<")
+    ora = _oracle_for(meta, 21, n_envs)
+    g, o = env.reset(4), ora.reset(4)
+    np.testing.assert_allclose(g[0], o[0], rtol=0, atol=F32_ATOL)
+    rng = np.random.default_rng(31)
+    # double integrator: envs driven all-done early (at a goal, zero acceleration) so their
+    # resets fall between the episode boundaries of the others
+    early = {13: (0, 5), 27: (3,), 44: (7, 8, 14), 58: (1,)} if dyn == "double_integrator" else {}
+    for t in range(75):
+        a = rng.integers(0, 25, (n_envs, N))
+        for k in early.get(t - 1, ()):
+            a[k] = 12
+        g = env.step(a, 4)
+        o = ora.step(a, 4)
+        ctx = "%s team %s step %d" % (dyn, team, t)
+        np.testing.assert_array_equal(g[5], o[5], err_msg=ctx)
+        np.testing.assert_array_equal(env.t_reset.cpu().numpy(), np.array([len(x) > N for x in o[6]]), err_msg=ctx)
+        np.testing.assert_array_equal(g[3] != 0, o[3] != 0, err_msg=ctx)
+        np.testing.assert_allclose(g[0], o[0], rtol=0, atol=F32_ATOL, err_msg=ctx)
+        np.testing.assert_allclose(g[2], o[2], rtol=0, atol=F32_ATOL, err_msg=ctx)
+        np.testing.assert_allclose(g[3], o[3], rtol=0, atol=F32_ATOL, err_msg=ctx)
+        np.testing.assert_allclose(g[4], o[4], rtol=1e-6, atol=1e-5, err_msg=ctx)
+        st = env.state().cpu().numpy()
+        for k, e in enumerate(ora.envs):
+            np.testing.assert_allclose(st[k], e.s, rtol=0, atol=STATE_ATOL, err_msg=ctx)
+        for k in early.get(t, ()):   # env k all-done at the next step (an off-phase reset)
+            s, r = _arrive_all(ora.envs[k])
+            env.set_agent_state(k, s, r)
+            e = ora.envs[k]
+            e.s[:] = s
+            e.reached_goal[:] = r
+            e.calculate_distances()
+    env.close()
