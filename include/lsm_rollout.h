@@ -169,8 +169,13 @@ const char* lsm_last_error(const lsm_env* env);
  * history: every reset whose curriculum separation differs from the env's current one applies
  * `values_hj -= shift` (float32 <- float64, HjDataHandle.update_separation_distance,
  * safety_filter.py:170-174) to that env only. At most 8 separation changes across the
- * reset/step calls' curriculum blocks are accepted per upload (lsm_step / lsm_reset fail
- * beyond that); uploading again starts every env's history afresh. */
+ * curriculum blocks of the calls that can reset (lsm_reset, lsm_reset_layout, lsm_step with
+ * auto_reset) are accepted per upload; beyond that those calls fail with nothing launched. The
+ * reference has no such bound. Recovery: upload the table again, shifted to the current
+ * separation (HjDataHandle(target_separation_distance = current)); that restarts every env's
+ * history from it, which differs from the reference's accumulated float32 shifts by at most the
+ * rounding of the dropped shifts (one float32 ulp of a value per shift). The training
+ * curriculum's stairs change the separation 4 times. */
 int lsm_set_value_table(lsm_env* env, int32_t ndim, const double* lo, const double* hi,
                         const int32_t* shape, const int32_t* periodic,
                         const float* values_host, const float* grads_host, double separation_distance);

@@ -103,16 +103,20 @@ struct TableDev {
 
 // Persistent per-env state: ONE contiguous record per env (env-major, 128-B aligned
 // stride) whose byte layout is exactly the head of the env's LDS block (lds_plan), so a
-// step starts with a straight float4 copy HBM -> LDS (one round trip) and ends with the
-// copy back. Record fields in order (16-B aligned each): ps [4][N], stats [NSTAT][N],
-// winfo [NWINFO][N], pdist, gmt, minrel, adiff [N] f64, done, reached, sfilt, decon [N]
-// i32, step i32 | cur [NCUR] f64, lm [6][NL] f64 (x, y, heading, speed, sin, cos) -- the
-// part after '|' changes only at reset and is written back only then.
+// step starts with a straight float4 copy HBM -> LDS and ends with the copy back. Fields
+// (16-B aligned each), in record order:
+//   [0, a1)   ps [4][N], pdist, adiff [N] f64, done, reached, sfilt, decon [N] i32, step i32
+//   [a1, a2)  cur [NCUR] + the HJ shift chain                               (reset only)
+//   [a2, a3)  stats [NSTAT][N], winfo [NWINFO][N], gmt, minrel [N] f64
+//   [a3, rec) lm [6][NL] f64 (x, y, heading, speed, sin, cos), lmd            (reset only)
+// A step rewrites [0, a1) and [a2, a3). Everything a step needs before its distances is in
+// [0, a2) (state, done flags, curriculum, shifts): the team kernel loads that part first and
+// the rest while its agent wave filters and integrates (lsm_team.h).
 struct StateDev {
   float4* rec;          // [n][rec_stride16]
   uint32_t rec_stride16;
   uint32_t rec16;       // float4 per record
-  uint32_t hot16;       // float4 rewritten every step (up to cur)
+  uint32_t a1_16, a2_16, a3_16;   // the boundaries above, in float4
   double* prev;         // [n][8] previous episode summary
   uint32_t* mt;         // [n][MT_WORDS] (LSM_RNG_PHILOX: only word MT_N, the reset index + MT_N)
   double* dep;          // [n][DEPW(N)] departed [N], departure_timer [N], init_theta [N], and the
@@ -266,7 +270,7 @@ __host__ __device__ inline size_t dep_lds_bytes(int N) {
 struct LdsPlan {
   size_t bytes;     // LDS per env
   size_t rec;       // persistent record bytes (LDS head == HBM record)
-  size_t hot;       // record bytes rewritten every step (fields before cur)
+  size_t a1, a2, a3;   // record sections (StateDev)
   size_t off[40];
 };
 
@@ -354,12 +358,25 @@ __host__ __device__ inline LdsPlan lds_plan(int N, int NL, int E, int F, bool bl
   size_t o = 0;
   int k = 0;
   auto put = [&](size_t bytes) { p.off[k++] = o; o += align16(bytes); };
-  // record
-  put(8 * 4 * N); put(8 * NSTAT * N); put(8 * NWINFO * N);
-  put(8 * N); put(8 * N); put(8 * N); put(8 * N);
-  put(4 * N); put(4 * N); put(4 * N); put(4 * N); put(8);
-  p.hot = o;
-  put(8 * (NCUR + NSEPW)); put(8 * 6 * NL); put(block ? 0 : 4 * (NL * (NL - 1) / 2));
+  // record: fields 0..14 (carve order: ps stats winfo pdist gmt minrel adiff done reached sfilt
+  // decon step cur lm lmd) placed in the section order of StateDev
+  {
+    const size_t fsz[15] = {(size_t)8 * 4 * N, (size_t)8 * NSTAT * N, (size_t)8 * NWINFO * N, (size_t)8 * N,
+                            (size_t)8 * N, (size_t)8 * N, (size_t)8 * N, (size_t)4 * N, (size_t)4 * N,
+                            (size_t)4 * N, (size_t)4 * N, 8, (size_t)8 * (NCUR + NSEPW), (size_t)8 * 6 * NL,
+                            block ? 0 : (size_t)4 * (NL * (NL - 1) / 2)};
+    const int order[15] = {0, 3, 6, 7, 8, 9, 10, 11, 12, 1, 2, 4, 5, 13, 14};
+#pragma unroll
+    for (int q = 0; q < 15; ++q) {
+      const int f = order[q];
+      p.off[f] = o;
+      o += align16(fsz[f]);
+      if (f == 11) p.a1 = o;
+      if (f == 12) p.a2 = o;
+      if (f == 5) p.a3 = o;
+    }
+    k = 15;
+  }
   p.rec = o;
   const int MW = (E + 63) / 64;
   // scratch
@@ -2119,7 +2136,13 @@ __device__ __forceinline__ void store_state(const KParams& P, Lds& S, const unsi
     if (P.o.state) gptr(P.o.state)[((size_t)env * N + j) * 4 + c] = v;
   }
   esync<LPE>();
-  rec_copy<LPE>((const f32x4*)lbase, (GAS f32x4*)gptr(P.s.rec) + (size_t)env * P.s.rec_stride16, full ? P.s.rec16 : P.s.hot16);
+  GAS f32x4* rg = (GAS f32x4*)gptr(P.s.rec) + (size_t)env * P.s.rec_stride16;
+  if (full) {
+    rec_copy<LPE>((const f32x4*)lbase, rg, P.s.rec16);
+  } else {   // the sections a step changes: [0, a1) and [a2, a3)
+    rec_copy<LPE>((const f32x4*)lbase, rg, P.s.a1_16);
+    rec_copy<LPE>((const f32x4*)lbase + P.s.a2_16, rg + P.s.a2_16, P.s.a3_16 - P.s.a2_16);
+  }
 }
 
 // integration of agent i, speed clamp, travel distance (core.py:118-131,199-210,680-687):
@@ -3158,7 +3181,9 @@ int lsm_create(const lsm_config* cfg, lsm_env** out) {
   int r = 0;
   const LdsPlan lp = lds_plan(N, e->NL, e->E, e->F, e->block);
   e->s.rec16 = (uint32_t)(lp.rec / 16);
-  e->s.hot16 = (uint32_t)(lp.hot / 16);
+  e->s.a1_16 = (uint32_t)(lp.a1 / 16);
+  e->s.a2_16 = (uint32_t)(lp.a2 / 16);
+  e->s.a3_16 = (uint32_t)(lp.a3 / 16);
   e->s.rec_stride16 = (uint32_t)(((lp.rec + 127) / 128) * 8);   // 128-B aligned records
   r |= dalloc(e, &e->s.rec, n * e->s.rec_stride16);
   r |= dalloc(e, &e->s.prev, n * 8);
@@ -3641,7 +3666,8 @@ int lsm_step(lsm_env* e, const void* actions, int32_t kind, const lsm_curriculum
   if (!e || !actions || !cur) return fail(e, "null argument");
   if (kind < 0 || kind > 2) return fail(e, "bad action kind");
   if (check_ready(e, true)) return 1;
-  if (sep_check(e, cur)) return 1;
+  // a step's curriculum block is used only by its auto-resets: without them no chain can grow
+  if (e->cfg.auto_reset && sep_check(e, cur)) return 1;
   KStep L;
   memset(&L, 0, sizeof(L));
   memcpy(L.cur_new, cur, sizeof(double) * NCUR);

@@ -204,6 +204,7 @@ void rollout_team_kernel(const KParams* __restrict__ Pp, const KStep K) {
 #endif
 
   // ---- A. record HBM -> LDS, actions, edges, decode, pair lookups --------------------------
+  const bool split = K.mode == 0 && !K.emit_edges;   // launch-uniform
   constexpr bool PRE = NT <= 8;
   constexpr int NPI = PRE ? ((NT * (NT - 1) / 2 + NT * 2 * NT) + LPE - 1) / LPE : 1;
   uint32_t prw[NPI];
@@ -219,7 +220,10 @@ void rollout_team_kernel(const KParams* __restrict__ Pp, const KStep K) {
         prw[k] = gptr(P.pairs)[t < E * (E - 1) / 2 ? t : 0];
       }
     }
-    rec_copy<LPE>((const GAS f32x4*)gptr(P.s.rec) + (size_t)env * P.s.rec_stride16, (f32x4*)lbase, P.s.rec16);
+    // a plain step needs [0, a2) of the record before its distances; the rest (statistics,
+    // landmarks) comes in phase B (cold_loads). Resets and the edge output read it all here.
+    rec_copy<LPE>((const GAS f32x4*)gptr(P.s.rec) + (size_t)env * P.s.rec_stride16, (f32x4*)lbase,
+                  split ? P.s.a2_16 : P.s.rec16);
     esync<LPE>();
     TSTAMP(12);
     if (lane < N) {
@@ -287,6 +291,18 @@ void rollout_team_kernel(const KParams* __restrict__ Pp, const KStep K) {
   TSTAMP(1);
 
   // ---- B. filter + integration, one lane per (env, agent) ------------------------------------
+  if (w != WB && split) {
+    // the record's [a2, rec) of every env of the workgroup, while HBM and these waves would
+    // otherwise idle; phase C is the first reader (landmarks), after the barrier below
+    const int c16 = (int)(P.s.rec16 - P.s.a2_16);
+    const int wi = w < WB ? w : w - 1;   // 0 .. G - 2 over the loading waves
+    for (int t = wi * 64 + lane; t < G * c16; t += (G - 1) * 64) {
+      const int g = t / c16, k = t - g * c16;
+      if (env0 + g < P.n_envs)
+        ((f32x4*)(smem + (size_t)g * B))[P.s.a2_16 + k] =
+            ((const GAS f32x4*)gptr(P.s.rec) + (size_t)(env0 + g) * P.s.rec_stride16)[P.s.a2_16 + k];
+    }
+  }
   if (w == WB) {
     if (alane) filter_agent_slot<DYN, NT>(P, A, N, ai, A.cur[C_FILT] != 0.0);
     esync<LPE>();   // every filter of the env has read the pre-step state

@@ -68,7 +68,9 @@ def main():
         env.step(act, 4)
         torch.cuda.synchronize()
         if t >= 10:
-            s = stamps.cpu().numpy().astype(np.float64)
+            raw = stamps.cpu().numpy()
+            hw = raw[:, 15].astype(np.uint64)   # HW_ID | XCC_ID << 32 of this step's waves
+            s = raw.astype(np.float64)
             tstamps.append(s[:, :9].copy())
             tstamps12.append(s[:, :13].copy())
             stamps.zero_()
@@ -87,6 +89,18 @@ def main():
             print("%-18s %12.0f   %5.1f%%  %8.0f" % (name, np.median(v), 100 * np.median(v) / tot,
                                                       np.percentile(v, 90)))
         print("%-18s %12.0f" % ("total", tot))
+        # per wave slot (env % G): phase medians and end time; and the slowest 2 % of waves
+        G = int(os.environ.get("LSM_TEAM", "4"))
+        slots = np.concatenate([np.arange(x.shape[0]) % G for x in tstamps])
+        rts = np.concatenate([x[:, 1] for x in rt])   # end (ns since the launch's first wave start)
+        print("slot   " + " ".join("%10s" % n[:10] for n, _, _ in segs) + "      end us")
+        for w in range(G):
+            m = slots == w
+            print("%-6d " % w + " ".join("%10.0f" % np.median(allst[m, j] - allst[m, i]) for _, i, j in segs) +
+                  "  %10.2f" % (np.median(rts[m]) / 1e3))
+        late = rts >= np.percentile(rts, 98)
+        print("late2% " + " ".join("%10.0f" % np.median(allst[late, j] - allst[late, i]) for _, i, j in segs) +
+              "  %10.2f  slots %s" % (np.median(rts[late]) / 1e3, np.bincount(slots[late], minlength=G).tolist()))
         ag = np.concatenate(tstamps12, axis=0)
         for name, i, j in [("A record", 0, 12), ("A decode+pairs", 12, 6), ("B filter", 1, 9),
                            ("B integrate", 9, 2), ("D reward", 3, 10),
@@ -108,7 +122,6 @@ def main():
     print("wave start  ", q(r[..., 0].ravel()))
     print("wave end    ", q(r[..., 1].ravel()))
     print("wave life   ", q((r[..., 1] - r[..., 0]).ravel()))
-    hw = stamps.cpu().numpy()[:, 15].astype(np.uint64)
     xcc = (hw >> np.uint64(32)) & np.uint64(0xf)
     hid = hw & np.uint64(0xffffffff)
     simd = (hid >> np.uint64(4)) & np.uint64(3)
@@ -126,6 +139,22 @@ def main():
     wv = [life[inv == k] for k in range(len(u))]
     c = np.corrcoef(cnt[inv], life)[0, 1] if cnt.min() != cnt.max() else float("nan")
     print("corr(waves on SIMD, life) %.2f" % c)
+    if a.team:
+        # SIMD placement of each wave slot w of the team workgroups (env = G * block + w), and how
+        # many distinct SIMDs the agent-phase waves (w = 0 for B, w = 1 for D) of one CU occupy
+        G = int(os.environ.get("LSM_TEAM", "4"))
+        slot = np.arange(len(simd)) % G
+        cukey = xcc * np.uint64(1000) + se * np.uint64(100) + cu
+        for w in range(G):
+            h = np.bincount(simd[slot == w].astype(np.int64), minlength=4)
+            print("wave slot %d: SIMD histogram %s" % (w, h.tolist()))
+        for w in (0, 1 % G):
+            m = slot == w
+            ks, inv2 = np.unique(cukey[m], return_inverse=True)
+            nd = [len(np.unique(simd[m][inv2 == k])) for k in range(len(ks))]
+            nw = np.bincount(inv2)
+            print("slot %d waves per CU: %s; distinct SIMDs among them: %s" % (
+                w, np.bincount(nw).nonzero()[0].tolist(), np.bincount(nd).tolist()))
     env.close()
 
 

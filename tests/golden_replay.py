@@ -50,8 +50,26 @@ def layout_for(meta):
     return lay, m
 
 
+class _Fixture(dict):
+    """An npz fixture whose arrays are read (decompressed) once, on first access: NpzFile
+    re-reads a member from the archive on every z[key], which per-step replays multiply."""
+
+    def __init__(self, z):
+        super().__init__()
+        self._z = z
+        self.files = z.files
+
+    def __missing__(self, key):
+        v = self._z[key]
+        self[key] = v
+        return v
+
+    def __contains__(self, key):
+        return key in self.files
+
+
 def load(name):
-    z = np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False)
+    z = _Fixture(np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False))
     meta = ast.literal_eval(str(z["meta"]))
     return z, meta
 
