@@ -107,7 +107,11 @@ def load_library(path: str = LIB_PATH):
         "lsm_episode_summary": (I32, [P, I32, P, P]),
     }
     for name, (res, args) in sig.items():
-        fn = getattr(lib, name)
+        fn = getattr(lib, name, None)
+        if fn is None and os.environ.get("LSM_LIB"):
+            continue   # an older library under A/B (tools/ab_bench.py) lacks a newer entry point
+        if fn is None:
+            raise AttributeError("%s: missing symbol %s" % (path, name))
         fn.restype = res
         fn.argtypes = args
     _lib = lib

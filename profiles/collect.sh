@@ -9,7 +9,7 @@ set -euo pipefail
 ROUND=${1:-r01}
 CFG=${2:-3}
 ROOT=$(pwd)
-OUT=$ROOT/gpurun_out/prof_${ROUND}_c${CFG}
+OUT=${TMPDIR:-/tmp}/prof_${ROUND}_c${CFG}   # raw traces stay on the box (gpurun_out is capped at 64 MiB)
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 BENCH="bench.py --config $CFG --steps 200 --warmup 20 --no-cpu-baseline"
