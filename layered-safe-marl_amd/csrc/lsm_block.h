@@ -186,8 +186,13 @@ __device__ __forceinline__ void reset_block(const KParams& P, Lds& S, int env, c
   emit_graph_block<DYN, NT>(P, S, env);
 }
 
-template <int DYN, int NT>
-__global__ __launch_bounds__(BT) void rollout_block_kernel(const KParams* __restrict__ Pp, const KStep K) {
+// NIS1: num_internal_step == 1 (the training default), compiled without the inner loop. Config 5
+// went from 1240 to 1490 us per step (same-session A/B, profiles/r03_v14_bisect_c5.txt) when the
+// loop came in: 172 VGPRs instead of 165, so 2 waves per SIMD instead of 3. waves_per_eu(3) holds
+// the kernel to the 168 VGPRs of 3 waves.
+template <int DYN, int NT, bool NIS1>
+__global__ __launch_bounds__(BT) __attribute__((amdgpu_waves_per_eu(DYN == 0 ? 3 : 1)))
+void rollout_block_kernel(const KParams* __restrict__ Pp, const KStep K) {
   const KParams& P = *Pp;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int env = xcd_block(blockIdx.x, gridDim.x);
@@ -281,7 +286,8 @@ __global__ __launch_bounds__(BT) void rollout_block_kernel(const KParams* __rest
   const bool filter_on = S.cur[C_FILT] != 0.0;
   // World.step's inner loop (core.py:607-631): filter -> action_diff -> integrate, num_internal_step
   // times on the same raw actions
-  for (int it = 0; it < P.nis; ++it) {
+  const int nis = NIS1 ? 1 : P.nis;
+  for (int it = 0; it < nis; ++it) {
   if (filter_on) {
     const SepChain sc = sep_chain(S.sep);
     const int i = tid / TE, q = tid - (tid / TE) * TE;
@@ -429,7 +435,7 @@ __global__ __launch_bounds__(BT) void rollout_block_kernel(const KParams* __rest
   // ---- 4. integrate ------------------------------------------------------------------------
   if (tid < N && !inactive_pre(S, tid)) integrate_agent<DYN>(P, S, N, tid);
   __syncthreads();
-  if (DYN == 1 && it + 1 < P.nis) {   // the next inner filter's ego frame: the new headings
+  if (DYN == 1 && it + 1 < nis) {   // the next inner filter's ego frame: the new headings
     if (tid < N) {
       S.ecs[tid] = cos(S.ps[2 * N + tid]);
       S.ecs[N + tid] = sin(S.ps[2 * N + tid]);

@@ -3498,17 +3498,23 @@ static int launch_team_t(lsm_env* e, const KStep& L, size_t env_bytes, hipStream
   return 0;
 }
 
-extern "C++" template <int DYN, int NT>
-static int launch_block_t(lsm_env* e, const KStep& L, size_t env_lds, hipStream_t st) {
+extern "C++" template <int DYN, int NT, bool NIS1>
+static int launch_block_nis(lsm_env* e, const KStep& L, size_t env_lds, hipStream_t st) {
   static bool attr = false;   // LDS above the 64 KB default needs an explicit opt-in
   if (!attr && env_lds > 65536) {
-    HIPCHK(e, hipFuncSetAttribute((const void*)rollout_block_kernel<DYN, NT>,
+    HIPCHK(e, hipFuncSetAttribute((const void*)rollout_block_kernel<DYN, NT, NIS1>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)env_lds));
     attr = true;
   }
-  hipLaunchKernelGGL((rollout_block_kernel<DYN, NT>), dim3(e->cfg.num_envs), dim3(BT), env_lds, st,
+  hipLaunchKernelGGL((rollout_block_kernel<DYN, NT, NIS1>), dim3(e->cfg.num_envs), dim3(BT), env_lds, st,
                      active_params(e), L);
   return 0;
+}
+
+extern "C++" template <int DYN, int NT>
+static int launch_block_t(lsm_env* e, const KStep& L, size_t env_lds, hipStream_t st) {
+  return e->cfg.num_internal_step > 1 ? launch_block_nis<DYN, NT, false>(e, L, env_lds, st)
+                                      : launch_block_nis<DYN, NT, true>(e, L, env_lds, st);
 }
 
 static int launch(lsm_env* e, KStep& L, hipStream_t st) {

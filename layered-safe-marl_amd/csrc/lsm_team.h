@@ -204,7 +204,9 @@ void rollout_team_kernel(const KParams* __restrict__ Pp, const KStep K) {
 #endif
 
   // ---- A. record HBM -> LDS, actions, edges, decode, pair lookups --------------------------
-  const bool split = K.mode == 0 && !K.emit_edges;   // launch-uniform
+  // launch-uniform. The double integrator only: the airtaxi agent wave's phase B (closed-form
+  // integration) is too short to hide the second half (config 4: 400.7 -> 415.2 us split).
+  const bool split = DYN == 0 && K.mode == 0 && !K.emit_edges;
   constexpr bool PRE = NT <= 8;
   constexpr int NPI = PRE ? ((NT * (NT - 1) / 2 + NT * 2 * NT) + LPE - 1) / LPE : 1;
   uint32_t prw[NPI];
