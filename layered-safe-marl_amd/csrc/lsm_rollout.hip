@@ -941,15 +941,23 @@ __device__ __forceinline__ bool goal_reached_at(const Lds& S, int N, int NL, int
 // double_integrator_velocity_error_from_magnetic_field_reference (utils.py:276-349).
 // The 50-segment Biot-Savart sum is split over G lanes per agent (segments g, g+G, ...);
 // the G partial sums are combined in lane order (float64; ulp-level vs the reference's
-// sequential sum, reward tolerance). Called by ALL lanes; returns the penalty in lanes
-// lane < N (agent = lane), garbage elsewhere.
+// sequential sum, reward tolerance). Two halves: magnetic_partials_wave (all lanes of an env's
+// wave: the segment sums into part[0, 2 LPE)) and magnetic_penalty_agent (one lane per agent:
+// the sums combined, the reference heading, the penalty), so that the team kernel runs the
+// second half once for its G envs in the agent wave.
+template <int LPE>
+__device__ __forceinline__ int mag_lanes_per_agent(int N) {
+  int G = 1;
+  while (G * 2 * N <= LPE) G *= 2;
+  return G;
+}
+
 template <int LPE, int NT>
-__device__ __forceinline__ double magnetic_penalty_wave(const KParams& P, Lds& S, double* part) {
+__device__ __forceinline__ void magnetic_partials_wave(const KParams& P, const Lds& S, double* part) {
   const int lane = threadIdx.x & (LPE - 1);
   constexpr int DYN = 0;
   LSM_DIMS;
-  int G = 1;
-  while (G * 2 * N <= LPE) G *= 2;
+  const int G = mag_lanes_per_agent<LPE>(N);
   const int a = lane / G, g = lane - a * G;
   const bool act = a < N;
   const int ai = act ? a : 0;
@@ -979,10 +987,17 @@ __device__ __forceinline__ double magnetic_penalty_wave(const KParams& P, Lds& S
   }
   part[lane] = m0;
   part[LPE + lane] = m1;
-  esync<LPE>();
+}
+
+// agent i's penalty from the partial sums of its env's wave (LPE: that wave's width)
+template <int LPE, int NT>
+__device__ __forceinline__ double magnetic_penalty_agent(const KParams& P, const Lds& S, const double* part,
+                                                         int i) {
+  constexpr int DYN = 0;
+  LSM_DIMS;
+  const int G = mag_lanes_per_agent<LPE>(N);
   double pen = 0.0;
-  if (lane < N) {
-    const int i = lane;
+  {
     const int gj = goal_index(S.rpre[i], i, N, NL);
     const double gxx = S.lm[gj], gyy = S.lm[NL + gj], ghh = S.lm[2 * NL + gj], gs = S.lm[3 * NL + gj];
     const double c = cos(ghh), s = sin(ghh);
@@ -1014,6 +1029,18 @@ __device__ __forceinline__ double magnetic_penalty_wave(const KParams& P, Lds& S
       pen = err * (1 - ar) + dist * ar;
     }
   }
+  return pen;
+}
+
+// Called by ALL lanes; returns the penalty in lanes lane < N (agent = lane), 0 elsewhere.
+template <int LPE, int NT>
+__device__ __forceinline__ double magnetic_penalty_wave(const KParams& P, Lds& S, double* part) {
+  const int lane = threadIdx.x & (LPE - 1);
+  constexpr int DYN = 0;
+  LSM_DIMS;
+  magnetic_partials_wave<LPE, NT>(P, S, part);
+  esync<LPE>();
+  const double pen = lane < N ? magnetic_penalty_agent<LPE, NT>(P, S, part, lane) : 0.0;
   esync<LPE>();
   return pen;
 }

@@ -14,7 +14,7 @@
 // Phases (W = workgroup barrier; every wave reaches each W the same number of times):
 //   A  (each env's wave)   record HBM -> LDS, actions, update_graph edges, decode, HJ pair lookups
 //   W  B (agent wave 0)    filter per agent, integrate                  (core.py:648-687)
-//   W  C (each env's wave) E x E distances, contact forces, magnetic field sums (filter off)
+//   W  C (each env's wave) E x E distances, contact forces, magnetic field segment sums (filter off)
 //   W  D (agent wave 1%G)  min relative distance, obs / reward / goal update, disconnect masks,
 //                          info, episode stats;   other waves: speculative adjacency stores
 //   W  E (each env's wave) info rows out, dones / masks, then the auto-reset or the graph outputs
@@ -337,11 +337,9 @@ void rollout_team_kernel(const KParams* __restrict__ Pp, const KStep K) {
       cf[0] = fx;
       cf[1] = fy;
     }
-    if (DYN == 0 && !P.use_filter_arg) {
-      // partial sums in U2; the per-agent result parks in wnew (info_agent's, written after use)
-      const double mag = magnetic_penalty_wave<LPE, NT>(P, S, S.dpair);
-      if (lane < N) S.wnew[lane] = mag;
-    }
+    // the magnetic-field segment sums (partials in U2, read by the agent wave in D, before the
+    // info rows reuse U2)
+    if (DYN == 0 && !P.use_filter_arg) magnetic_partials_wave<LPE, NT>(P, S, S.dpair);
     m_pre = chunked ? ego_mask(S, N, L, -1) : 0;
   }
   TSTAMP(7);
@@ -356,7 +354,8 @@ void rollout_team_kernel(const KParams* __restrict__ Pp, const KStep K) {
     AgentTmp at;
     if (alane) {
       min_relative(A, N, ai);
-      const double mag = (DYN == 0 && !P.use_filter_arg) ? A.wnew[ai] : 0.0;
+      // the per-agent half of the magnetic penalty, once for the G envs (was 4 env waves in C)
+      const double mag = (DYN == 0 && !P.use_filter_arg) ? magnetic_penalty_agent<LPE, NT>(P, A, A.dpair, ai) : 0.0;
       reward_agent<DYN, NT>(P, A, aenv, ai, mag, at);
     }
     esync<LPE>();   // every agent's goal / done update before the snapshot masks
