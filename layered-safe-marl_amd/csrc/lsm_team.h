@@ -415,7 +415,11 @@ void rollout_team_kernel(const KParams* __restrict__ Pp, const KStep K) {
     int p0 = 0;
     if (rs) p0 = team_reset_prep<DYN, NT>(P, S, env, K.cur_new);
     __syncthreads();
+#ifdef LSM_XP_SCEN_PERWAVE
+    if (rs && lane == 0) team_scenario<DYN, NT>(P, smem, B, w, env);
+#else
     if (w == 0 && lane < G && team_rs[lane]) team_scenario<DYN, NT>(P, smem, B, lane, env0 + lane);
+#endif
     __syncthreads();
     if (rs) {
       team_reset_finish<DYN, NT>(P, S, env, p0);
