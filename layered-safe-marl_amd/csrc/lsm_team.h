@@ -415,11 +415,9 @@ void rollout_team_kernel(const KParams* __restrict__ Pp, const KStep K) {
     int p0 = 0;
     if (rs) p0 = team_reset_prep<DYN, NT>(P, S, env, K.cur_new);
     __syncthreads();
-#ifdef LSM_XP_SCEN_PERWAVE
-    if (rs && lane == 0) team_scenario<DYN, NT>(P, smem, B, w, env);
-#else
+    // (each env's wave drawing its own env on one lane measured slower: reset steps 85.7-89.1 vs
+    // 79.8-85.9 us, profiles/r03_v19_reset_*.json)
     if (w == 0 && lane < G && team_rs[lane]) team_scenario<DYN, NT>(P, smem, B, lane, env0 + lane);
-#endif
     __syncthreads();
     if (rs) {
       team_reset_finish<DYN, NT>(P, S, env, p0);
