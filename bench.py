@@ -189,6 +189,28 @@ def launch(a):
     return bad[0] if bad else 0
 
 
+_M1, _M2, _GOLD = -4658895280553007687, -7723592293110705685, -7046029254386353131   # splitmix64 constants
+
+
+def _mix64(x):
+    """splitmix64's finaliser on int64 tensors (wrapping multiplies; logical shifts by masking)."""
+    x = x ^ ((x >> 30) & 0x3FFFFFFFF)
+    x = x * _M1
+    x = x ^ ((x >> 27) & 0x1FFFFFFFFF)
+    x = x * _M2
+    return x ^ ((x >> 31) & 0x1FFFFFFFF)
+
+
+def synthetic_actions(t, env0, n_envs, N, device):
+    """Discrete(25) action indices of step t for global envs [env0, env0 + n_envs) (int32 [n_envs, N]):
+    a hash of (step, global env, agent), so any rank draws its own rows without the others'."""
+    import torch
+    idx = ((torch.arange(n_envs, device=device, dtype=torch.int64) + env0)[:, None] * N +
+           torch.arange(N, device=device, dtype=torch.int64)[None, :])
+    x = _mix64(idx * _GOLD + _mix64(torch.full_like(idx, 1234 + t)))
+    return (((x >> 33) & 0x7FFFFFFF) % 25).to(torch.int32)
+
+
 def timed_window(warmup, steps, epl):
     """Untimed steps before the timed window: at least `warmup`, and as many more as put an
     episode boundary (the auto-reset launch and the episode-summary collective) in the middle of
@@ -205,7 +227,8 @@ def dry_run(a, rank, world):
     c = CONFIGS[a.config]
     n_envs = a.envs or c["envs"]
     if world > 1:
-        dist.init_process_group("gloo")
+        from lsm.dist import init_rank
+        init_rank("gloo")
         assert dist.get_world_size() == a.gpus, (dist.get_world_size(), a.gpus)
     ep = torch.arange(n_envs * 8, dtype=torch.float64).reshape(n_envs, 8) + rank * n_envs * 8
     summ = global_episode_summary(ep)
@@ -278,15 +301,15 @@ def main():
 
     import torch
     import torch.distributed as dist
+    from lsm.dist import init_rank, barrier
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        dist.init_process_group(a.dist_backend)
-        if dist.get_world_size() != a.gpus:
-            raise SystemExit("%s world size %d != --gpus %d" % (a.dist_backend, dist.get_world_size(), a.gpus))
-    # one GPU per rank; the test-only gloo mode may put several ranks on one device
-    dev = torch.device("cuda:%d" % (local_rank % torch.cuda.device_count() if a.dist_backend == "gloo"
-                                    else local_rank))
-    torch.cuda.set_device(dev)
+    # one GPU per rank, bound BEFORE the process group (RCCL gets it as device_id): a communicator
+    # created first would bind every rank to GPU 0. The test-only gloo mode may share one device.
+    dev = init_rank(a.dist_backend, device_index=(local_rank % torch.cuda.device_count()
+                                                  if a.dist_backend == "gloo" else local_rank))
+    if world > 1 and dist.get_world_size() != a.gpus:
+        raise SystemExit("%s world size %d != --gpus %d" % (a.dist_backend, dist.get_world_size(), a.gpus))
     from lsm.vec_env import GpuGraphVecEnv
     layout = c.get("adj_layout", "reference")
     env = GpuGraphVecEnv(args, num_envs=n_envs, device=dev, value_table=vt, ttr_table=tt,
@@ -297,15 +320,11 @@ def main():
     pre = timed_window(a.warmup, a.steps, epl)
     # Synthetic policy: every step's discrete actions drawn up front, resident in HBM before the
     # timed region (the policy is outside the path; one env-step = one rollout_kernel launch).
-    # Step t's actions for ALL global envs come from one generator seeded 1234 + t and each rank
-    # keeps its slice, so a sharded run steps exactly the envs of a single-process run.
-    gen = torch.Generator(device=dev)
+    # A counter-based draw indexed by (step, global env, agent): each rank draws only its own rows,
+    # and a sharded run steps exactly the envs of a single-process run.
     acts_all = torch.empty((pre + a.steps, n_envs, N), dtype=torch.int32, device=dev)
     for t in range(pre + a.steps):
-        gen.manual_seed(1234 + t)
-        full = torch.randint(0, 25, (world * n_envs, N), generator=gen, device=dev, dtype=torch.int32)
-        acts_all[t].copy_(full[rank * n_envs:(rank + 1) * n_envs])
-    del full
+        acts_all[t].copy_(synthetic_actions(t, rank * n_envs, n_envs, N, dev))
     buf = None
     if a.buffer:
         from lsm.buffer import DeviceGraphBuffer
@@ -338,8 +357,7 @@ def main():
     # event pairs would add their own GPU-side markers between back-to-back launches).
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    barrier(a.dist_backend)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     ev0.record()
@@ -347,8 +365,7 @@ def main():
         one_step(pre + t)
     ev1.record()
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    barrier(a.dist_backend)
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     kern_ms = ev0.elapsed_time(ev1) / a.steps   # includes the inter-launch gaps (conservative)

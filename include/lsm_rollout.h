@@ -139,7 +139,26 @@ typedef struct lsm_config {
   int32_t num_internal_step; /* args.num_internal_step (0 or 1 = one): World.step repeats filter ->
                                 action_diff -> integrate this many times per env step, then the
                                 distances and minimum relative distance (core.py:607-631)         */
+  int32_t reward_terms;      /* LSM_REWARD_* bits: RewardBinaryConfig's optional reward terms
+                                (multiagent/config.py:78-83, all off by default), added in
+                                SafeAamScenario.reward (navigation_graph_safe.py:843-850). HJ_VALUE
+                                needs the value table (lsm_set_value_table) even with the filter off:
+                                the reference builds the HJ handle then (:195) and shifts it at every
+                                reset like the filter's (core.py:483-486). Unknown bits are refused. */
+  int32_t collaborative;     /* args.collaborative: MultiAgentGraphEnv.shared_reward
+                                (environment.py:79-80) -- every agent's LSM_OUT_REWARD entry is the
+                                numpy sum of the env's individual rewards (:1031-1037); info
+                                'individual_reward' keeps each agent's own                        */
 } lsm_config;
+
+/* lsm_config.reward_terms bits (RewardBinaryConfig, multiagent/config.py:78-83) */
+enum {
+  LSM_REWARD_SAFETY_VIOLATION = 1,            /* reward_safety_violation, navigation_graph_safe.py:793-798 */
+  LSM_REWARD_POTENTIAL_CONFLICT = 2,          /* reward_multiple_engagement, :800-823                    */
+  LSM_REWARD_DIFF_FROM_FILTERED_ACTION = 4,   /* reward_diff_from_filtered_action, :825-828 (filter on)  */
+  LSM_REWARD_HJ_VALUE = 8,                    /* reward_hj_value, :830-837 (World.get_hj_value..., core.py:459) */
+  LSM_REWARD_ALL = 15
+};
 
 /* Curriculum block for one reset call (navigation_graph_safe.py:324-366), computed by the
  * host with the reference's own float64 expressions. */
@@ -155,7 +174,10 @@ typedef struct lsm_curriculum {
   double separation_distance;
   double engagement_distance;
   double world_use_safety_filter; /* 0/1 */
-  double reserved;
+  double stair_is_int;       /* 1 when get_effective_curriculum_ratio_stair() returned the Python int
+                                0 or 1 (ratio outside [start, end], :1115-1118), else 0: the scaled
+                                reward weights (:340-345) are then Python ints, and an int times a
+                                float32 HJ value stays float32 (reward_hj_value's sums)           */
 } lsm_curriculum;
 
 int lsm_create(const lsm_config* cfg, lsm_env** out);
@@ -168,14 +190,11 @@ const char* lsm_last_error(const lsm_env* env);
  * target_separation_distance, safety_filter.py:155-168). Each env then keeps its own table
  * history: every reset whose curriculum separation differs from the env's current one applies
  * `values_hj -= shift` (float32 <- float64, HjDataHandle.update_separation_distance,
- * safety_filter.py:170-174) to that env only. At most 8 separation changes across the
- * curriculum blocks of the calls that can reset (lsm_reset, lsm_reset_layout, lsm_step with
- * auto_reset) are accepted per upload; beyond that those calls fail with nothing launched. The
- * reference has no such bound. Recovery: upload the table again, shifted to the current
- * separation (HjDataHandle(target_separation_distance = current)); that restarts every env's
- * history from it, which differs from the reference's accumulated float32 shifts by at most the
- * rounding of the dropped shifts (one float32 ulp of a value per shift). The training
- * curriculum's stairs change the separation 4 times. */
+ * safety_filter.py:170-174) to that env only, every shift rounded to float32 in turn as numpy does.
+ * The chain has no length bound: its first 8 shifts live in the env's record, later ones in a
+ * per-env HBM array that a call which can reset (lsm_reset, lsm_reset_layout, lsm_step with
+ * auto_reset) grows before its launch when the number of separation changes since the upload needs
+ * it (one stream synchronisation then). Needed with the filter on, or with LSM_REWARD_HJ_VALUE. */
 int lsm_set_value_table(lsm_env* env, int32_t ndim, const double* lo, const double* hi,
                         const int32_t* shape, const int32_t* periodic,
                         const float* values_host, const float* grads_host, double separation_distance);

@@ -289,7 +289,7 @@ void rollout_block_kernel(const KParams* __restrict__ Pp, const KStep K) {
   const int nis = NIS1 ? 1 : P.nis;
   for (int it = 0; it < nis; ++it) {
   if (filter_on) {
-    const SepChain sc = sep_chain(S.sep);
+    const SepChain sc = sep_chain(S.sep, P.s, env);
     const int i = tid / TE, q = tid - (tid / TE) * TE;
     int jd = -1, jv = -1, okv = 0;
     double dmin = 0.0;
@@ -488,6 +488,12 @@ void rollout_block_kernel(const KParams* __restrict__ Pp, const KStep K) {
   AgentTmp at;
   if (tid < N) reward_agent<DYN, NT>(P, S, env, tid, mag, at);
   __syncthreads();
+  if (P.rext) {   // optional reward terms / shared reward (reward_finish)
+    if (tid < N) reward_finish<DYN, NT>(P, S, env, tid, at);
+    __syncthreads();
+    if (P.collab && tid < N) reward_shared<NT>(P, S, env, tid);
+    __syncthreads();
+  }
   mask_words(S, N, E);
   __syncthreads();
   for (int k = tid; k < N * MW; k += BT) {

@@ -149,6 +149,7 @@ struct HostMT {
     if (pos >= MT_N) gen();
     return mt_temper(key[pos++]);
   }
+  bool exhausted() const { return false; }
   double next_double() {
     uint32_t a = next32() >> 5, b = next32() >> 6;
     return (a * 67108864.0 + b) / 9007199254740992.0;
@@ -195,6 +196,7 @@ struct Philox {
     if (pos >= 4) round_all();
     return buf[pos++];
   }
+  LSM_HD bool exhausted() const { return false; }
   LSM_HD double next_double() {
     uint32_t a = next32() >> 5, b = next32() >> 6;
     return (a * 67108864.0 + b) / 9007199254740992.0;

@@ -38,6 +38,21 @@
 #include "lsm_rk45.h"
 #include "lsm_scenario.h"
 
+// Diagnostic switches (bounds that compute wrong results on purpose, in-kernel stamps) exist only in
+// variant builds (lsm.build.build_variants defines LSM_DIAGNOSTIC_BUILD); the product refuses them.
+#if !defined(LSM_DIAGNOSTIC_BUILD) &&                                                              \
+    (defined(LSM_STAMPS) || defined(LSM_XP_VALHOT) || defined(LSM_XP_GRADHOT) || defined(LSM_XP_NOFILT) || \
+     defined(LSM_XP_NOOUT) || defined(LSM_XP_NORESETEMIT) || defined(LSM_XP_NORK) || defined(LSM_XP_NOSCEN))
+#error "diagnostic switch in a product build: use lsm.build.build_variants (LSM_DIAGNOSTIC_BUILD)"
+#endif
+
+// LSM_PART (lsm.build): 0 = host code only, g > 0 = kernel group g only, undefined = everything
+#if defined(LSM_PART) && LSM_PART != 0
+#define LSM_HOST_PART 0
+#else
+#define LSM_HOST_PART 1
+#endif
+
 #ifdef LSM_STAMPS
 // diagnostic build only: per-phase s_memtime stamps of each env's wave (never in the product .so)
 #define STAMP(k)                                                                             \
@@ -74,7 +89,9 @@ constexpr int NWINFO = 4;       // times_required, dists_to_goal, dist_left_to_g
 // (safety_filter.py:170-174) runs `values_hj -= shift` on every reset of every env, so each env's
 // table is the uploaded one minus its own chain of float64 shifts, each rounded to float32
 // (numpy: float32 array -= float64 scalar). sep[0] = number of shifts, sep[1] = the env's current
-// separation (sep[0] == 0: the uploaded table's, KParams::val_sep0), sep[2 + k] = shift k.
+// separation (sep[0] == 0: the uploaded table's, KParams::val_sep0), sep[2 + k] = shift k for
+// k < KSEP; longer chains continue in StateDev::sepx (HBM, grown by the host as the number of
+// separation changes since the upload grows), so no length is refused.
 constexpr int KSEP = 8;
 constexpr int NSEPW = 2 + KSEP;
 
@@ -121,6 +138,8 @@ struct StateDev {
   uint32_t* mt;         // [n][MT_WORDS] (LSM_RNG_PHILOX: only word MT_N, the reset index + MT_N)
   double* dep;          // [n][DEPW(N)] departed [N], departure_timer [N], init_theta [N], and the
                         // final disconnect mask of the last call (u64 bits) (LSM_SCENARIO_DEPARTURES)
+  double* sepx;         // [n][sepx_cap] HJ separation shifts KSEP, KSEP + 1, ... of each env's chain
+  uint32_t sepx_cap;    // (nullptr / 0 until a chain can outgrow the record's KSEP slots)
 };
 
 struct OutDev {
@@ -150,6 +169,12 @@ struct KParams {
   int scenario;      // LSM_SCENARIO_*
   int rng;           // LSM_RNG_*
   int nis;           // World.num_internal_step (>= 1): filter -> integrate repeats per step
+  int rbin;          // lsm_config.reward_terms (LSM_REWARD_* bits)
+  int collab;        // lsm_config.collaborative: shared reward
+  int rext;          // rbin || collab: rewards finished after every agent's goal / done update
+  int use_hj;        // the HJ handle exists (filter on, or LSM_REWARD_HJ_VALUE): resets shift it
+  int mt_stage;      // team-kernel resets: MT19937 words one lane may draw from the staged blocks
+                     // (2 MT_N; LSM_MT_STAGE lowers it so tests reach the cooperative redraw)
   int64_t seed, env_offset;   // Philox keys: seed + 1000 * (env_offset + env)
   uint32_t lds_dep_off;       // LSM_SCENARIO_DEPARTURES: LDS offset of the departure arrays
   double dt, world_size, coord_range, world_eng, sep_target, max_speed, min_speed, gs_min, gs_max;
@@ -560,7 +585,7 @@ __device__ __forceinline__ Lds carve_block(unsigned char* base, int N, int NL, i
   return L;
 }
 
-enum { C_CR = 0, C_SLOPED, C_STAIR, C_RAT, C_RSC, C_GHE, C_GSE, C_MDT, C_SEP, C_ENG, C_FILT };
+enum { C_CR = 0, C_SLOPED, C_STAIR, C_RAT, C_RSC, C_GHE, C_GSE, C_MDT, C_SEP, C_ENG, C_FILT, C_SINT };
 
 // ----------------------------------------------------------------------------------
 // Wave-cooperative MT19937 (numpy legacy stream); all lanes run the same scalar sequence.
@@ -608,6 +633,7 @@ struct WaveRng {
     pos++;
     return mt_temper(y);
   }
+  __device__ __forceinline__ bool exhausted() const { return false; }
   __device__ __forceinline__ double next_double() {
     uint32_t a = next32() >> 5;
     uint32_t b = next32() >> 6;
@@ -681,23 +707,27 @@ __device__ __forceinline__ bool grid_cell(const TableDev& T, const double* s, in
 // each shift in turn, float64 subtraction rounded to float32 (`values_hj -= shift`,
 // safety_filter.py:173, a float32 array minus a numpy float64 scalar).
 struct SepChain {
-  const double* sh;   // shifts in application order
+  const double* sh;   // shifts in application order: [0, KSEP) in the record (LDS) ...
   int n;
+  const double* shx;  // ... the rest in the env's HBM overflow row (StateDev::sepx)
   __device__ __forceinline__ float apply(float v) const {
-    for (int k = 0; k < n; ++k) v = (float)((double)v - sh[k]);
+    const int n0 = n < KSEP ? n : KSEP;
+    for (int k = 0; k < n0; ++k) v = (float)((double)v - sh[k]);
+    for (int k = KSEP; k < n; ++k) v = (float)((double)v - ((const GAS double*)shx)[k - KSEP]);
     return v;
   }
 };
-__device__ __forceinline__ SepChain sep_chain(const double* sep) {
+__device__ __forceinline__ SepChain sep_chain(const double* sep, const StateDev& sd, int env) {
   SepChain c;
   c.n = (int)sep[0];
   c.sh = sep + 2;
+  c.shx = sd.sepx ? sd.sepx + (size_t)env * sd.sepx_cap : nullptr;
   return c;
 }
 
 template <int ND>
 __device__ __forceinline__ bool interp_value(const TableDev& T, const double* s, float& out,
-                                             SepChain sc = SepChain{nullptr, 0}) {
+                                             SepChain sc = SepChain{nullptr, 0, nullptr}) {
   int cell;
   float w[1 << ND];
   if (!grid_cell<ND>(T, s, cell, w)) return false;
@@ -753,7 +783,7 @@ __device__ __forceinline__ void interp_grad(const TableDev& T, const double* s, 
 // (the lookup is +inf, no load).
 template <int ND>
 __device__ __forceinline__ bool value_bounds(const TableDev& T, const double* s, float2& b,
-                                             SepChain sc = SepChain{nullptr, 0}) {
+                                             SepChain sc = SepChain{nullptr, 0, nullptr}) {
   int blk = 0;
 #pragma unroll
   for (int d = 0; d < ND; ++d) {
@@ -784,6 +814,7 @@ __device__ __forceinline__ bool value_bounds(const TableDev& T, const double* s,
   return true;
 }
 
+#if LSM_HOST_PART
 // One thread per bounds block: min / max over the nodes its cells interpolate (cells
 // [b B, (b + 1) B) per dim -> nodes [b B, (b + 1) B] clipped, wrapped on periodic dims),
 // widened by 4e-6 max|v|: the fp32 sum of 2^d weighted corners stays within ~20 ulp of
@@ -822,7 +853,9 @@ __global__ void bounds_kernel(const float* values, float2* bnd, TableDev T, int 
   const float m = 4.0e-6f * fmaxf(fabsf(mn), fabsf(mx));
   bnd[b] = make_float2(mn - m, mx + m);
 }
+#endif
 
+#if LSM_HOST_PART
 // Expand a node table into the cell-corner layout (one thread per (cell, corner)).
 __global__ void expand_cells_kernel(const float* values, const float4* grads, float* cells, float4* gcells,
                                     TableDev T, int64_t n_cells) {
@@ -849,6 +882,7 @@ __global__ void expand_cells_kernel(const float* values, const float4* grads, fl
   if (grads)
     for (int q = 0; q < T.gw; ++q) gcells[t * T.gw + q] = grads[node * T.gw + q];
 }
+#endif
 
 // ----------------------------------------------------------------------------------
 // per-agent helpers
@@ -1958,16 +1992,18 @@ __device__ __forceinline__ void reset_head(const KParams& P, Lds& S, int env, co
   }
   esync<LPE>();
   for (int k = lane; k < NCUR; k += LPE) S.cur[k] = cur_new[k];
-  if (lane == 0 && P.use_filter_arg) {
+  if (lane == 0 && P.use_hj) {
     // update_curriculum -> world.update_safety_filter_separation_distance -> HjDataHandle.
     // update_separation_distance (navigation_graph_safe.py:363-364, core.py:483-486,
     // safety_filter.py:170-174): shift = target - previous in float64; a zero shift leaves the
-    // table unchanged. The host bounds the chain length (lsm_step / lsm_reset refuse > KSEP).
+    // table unchanged. Shifts past the record's KSEP slots go to the env's overflow row, which the
+    // host has sized for every chain the launch can produce (sep_check).
     const int n = (int)S.sep[0];
     const double prev = n ? S.sep[1] : P.val_sep0;
     const double sh = cur_new[C_SEP] - prev;
-    if (sh != 0.0 && n < KSEP) {
-      S.sep[2 + n] = sh;
+    if (sh != 0.0) {
+      if (n < KSEP) S.sep[2 + n] = sh;
+      else gptr(P.s.sepx)[(size_t)env * P.s.sepx_cap + (n - KSEP)] = sh;
       S.sep[0] = (double)(n + 1);
       S.sep[1] = cur_new[C_SEP];
     }
@@ -2376,9 +2412,11 @@ __device__ __forceinline__ void collision_force_agent(const Lds& S, int N, int i
 }
 
 // Per-agent values of the reward phase that the info phase reuses.
+// `base`: reward_reach_goal's value before the clip, a Python int 0 (base_int) when no float term
+// entered it (the agent was done and got no goal reward); reward_finish adds the optional terms.
 struct AgentTmp {
-  double rew = 0.0, th_pre = 0.0, spd_pre = 0.0, ct_pre = 1.0, st_pre = 0.0;
-  bool reached_pre = false;
+  double rew = 0.0, th_pre = 0.0, spd_pre = 0.0, ct_pre = 1.0, st_pre = 0.0, base = 0.0;
+  bool reached_pre = false, base_int = false;
 };
 
 // obs (before the update), reward, goal / done update of agent i (navigation_graph_safe.py:
@@ -2451,6 +2489,8 @@ __device__ __forceinline__ void reward_agent(const KParams& P, Lds& S, int env, 
       r = r - sen * cra;
     }
   }
+  t.base = r;
+  t.base_int = done0 && !(reached && !P.use_masking);
   t.rew = np_clip(r, -40.0, 50.0);
   if (DYN == 1 && S.dep0) {
     // RealisticScenario.update_reached_goal_and_done (navigation_graph_safe.py:1153-1186): the
@@ -2488,7 +2528,180 @@ __device__ __forceinline__ void reward_agent(const KParams& P, Lds& S, int env, 
     S.rpost[i] = rp;
     S.dpost[i] = (rp >= L) ? 1 : S.dpre[i];
   }
-  gptr(P.o.rew)[(size_t)env * N + i] = (float)t.rew;
+  if (!P.rext) gptr(P.o.rew)[(size_t)env * N + i] = (float)t.rew;   // else reward_finish writes it
+}
+
+// ---- optional reward terms and the shared reward ---------------------------------------------
+// SafeAamScenario.reward adds RewardBinaryConfig's terms (navigation_graph_safe.py:793-850) to
+// reward_reach_goal before the clip, agent by agent: agent i's terms see agents a < i after their
+// goal / done update of this step and agents a > i before it. Run once every agent's update is in
+// LDS (reward_agent for all of the env's agents, then a sync), one lane per agent.
+//
+// The reference adds Python scalars of four kinds and numpy's promotion of them decides whether a
+// sum is rounded to float32: reward_hj_value's terms are np.float32 (a Python-int weight -- the
+// stair ratio is the int 0 or 1 outside its ramp -- times the JAX float32 value), np.int64 (np.abs
+// of the int 0 that min() returns) or np.float64 (a float64 weight). PyNum restates those
+// promotions (NumPy 2: Python scalars are weak; np.float32 + np.int64 is float64).
+enum { PY_INT = 0, NP_I64 = 1, NP_F32 = 2, NP_F64 = 3 };
+struct PyNum {
+  double v;
+  int t;
+};
+__device__ __forceinline__ PyNum py_num(double v, int t) {
+  PyNum r;
+  r.v = v;
+  r.t = t;
+  return r;
+}
+__device__ __forceinline__ PyNum py_add(PyNum a, PyNum b) {
+  int t;
+  if (a.t == NP_F64 || b.t == NP_F64) t = NP_F64;
+  else if (a.t == NP_F32 || b.t == NP_F32) t = (a.t == NP_I64 || b.t == NP_I64) ? NP_F64 : NP_F32;
+  else t = (a.t == NP_I64 || b.t == NP_I64) ? NP_I64 : PY_INT;
+  return py_num(t == NP_F32 ? (double)((float)a.v + (float)b.v) : a.v + b.v, t);
+}
+
+// agent j's state (x, y, v_x | theta, v_y | speed) as the reward of agent i sees it: `post` (j < i)
+// after j's update -- a freeze, or a RealisticScenario departure / waiting freeze
+template <int DYN>
+__device__ __forceinline__ void agent_state_seen(const Lds& S, int N, int j, bool post, double* s) {
+  s[0] = S.ps[j];
+  s[1] = S.ps[N + j];
+  if (DYN == 1 && post && S.psp) {
+    s[2] = S.pth[j];
+    s[3] = S.psp[j];
+    return;
+  }
+  const bool fz = post && froze_now(S, j);
+  s[2] = (DYN == 0 && fz) ? 0.0 : S.ps[2 * N + j];
+  s[3] = fz ? 0.0 : S.ps[3 * N + j];
+}
+
+// state.p_vel (core.py:106-108, 184-185)
+template <int DYN>
+__device__ __forceinline__ void p_vel(const double* s, double& vx, double& vy) {
+  if (DYN == 0) {
+    vx = s[2];
+    vy = s[3];
+  } else {
+    vx = s[3] * cos(s[2]);
+    vy = s[3] * sin(s[2]);
+  }
+}
+
+// reward_finish: agent i's optional terms, the clip, and its reward (individual, or kept in LDS for
+// the shared sum: S.raw[i] value, S.safe[i] its scalar kind -- both dead after the integration).
+template <int DYN, int NT>
+__device__ __forceinline__ void reward_finish(const KParams& P, Lds& S, int env, int i, AgentTmp& t) {
+  LSM_DIMS;
+  const bool wint = S.cur[C_SINT] != 0.0;          // the scaled weights are Python ints
+  const int wt = wint ? PY_INT : NP_F64;
+  const double st = S.cur[C_STAIR], sep = S.cur[C_SEP], eng = S.cur[C_ENG];
+  double si[4], vix, viy;
+  agent_state_seen<DYN>(S, N, i, false, si);
+  p_vel<DYN>(si, vix, viy);
+  PyNum sv = py_num(0.0, PY_INT), hj = py_num(0.0, PY_INT);
+  double me = 0.0;
+  int me_cnt = 0;
+  const SepChain sc = sep_chain(S.sep, P.s, env);
+  for (int a = 0; a < N; ++a) {
+    if (a == i) continue;
+    const bool post = a < i;
+    if ((post ? S.dpost[a] : S.dpre[a]) != 0) continue;   // every term skips done agents
+    double sa[4];
+    agent_state_seen<DYN>(S, N, a, post, sa);
+    const double rx = sa[0] - si[0], ry = sa[1] - si[1];   // a.p_pos - agent.p_pos
+    const double d = blas_norm2(rx, ry);                   // np.linalg.norm
+    // reward_safety_violation / is_confliction (:503-506, :793-798)
+    if ((P.rbin & LSM_REWARD_SAFETY_VIOLATION) && d < sep) sv = py_add(sv, py_num(-20.0 * st, wt));
+    // reward_multiple_engagement / is_in_engagement (:508-511, :800-823)
+    if ((P.rbin & LSM_REWARD_POTENTIAL_CONFLICT) && d < eng) {
+      const double close = 1 - np_clip((d - sep) / (eng - sep), 0, 1);
+      const double ang = atan2(ry, rx);
+      const double dx = cos(ang), dy = sin(ang);
+      double vax, vay;
+      p_vel<DYN>(sa, vax, vay);
+      const double ch = fma(dy, vay - viy, dx * (vax - vix));   // np.inner (BLAS ddot)
+      me += (ch < 0 ? -ch : 0.0) * close;                       // np.abs(min(0, change)) * closeness
+      ++me_cnt;
+    }
+    // reward_hj_value (:830-837): World.get_hj_value_between_two_agents(agent, a) (core.py:459-468)
+    if (P.rbin & LSM_REWARD_HJ_VALUE) {
+      double rel[5];
+      if (DYN == 0) {
+        for (int k = 0; k < 4; ++k) rel[k] = si[k] - sa[k];
+      } else {   // KinematicVehicleSafetyHandle.get_relative_state (safety_filter.py:277-284)
+        const double ox = sa[0] - si[0], oy = sa[1] - si[1];
+        const double dd = sqrt(ox * ox + oy * oy);
+        const double al = atan2(oy, ox);
+        rel[0] = dd * cos(al - si[2]);
+        rel[1] = dd * sin(al - si[2]);
+        rel[2] = sa[2] - si[2];
+        rel[3] = si[3];
+        rel[4] = sa[3];
+      }
+      float v = 0.0f;
+      const bool ok = DYN == 0 ? interp_value<4>(P.val, rel, v, sc) : interp_value<5>(P.val, rel, v, sc);
+      // np.abs(min(value - eps_hj, 0)): the float32 |value - 0.4| when it is <= 0, else np.int64 0
+      // (min returns its int 0; out of the grid the value is +inf)
+      const float x = v - 0.4f;
+      const PyNum pen = (ok && !(x > 0.0f)) ? py_num((double)fabsf(x), NP_F32) : py_num(0.0, NP_I64);
+      const double w = -2.0 * st;
+      PyNum term;   // conflict_value_rew_scaled * pen
+      if (wint) term = py_num(pen.t == NP_F32 ? (double)((float)w * (float)pen.v) : w * pen.v, pen.t);
+      else term = py_num(w * pen.v, NP_F64);
+      hj = py_add(hj, term);
+    }
+  }
+  PyNum rew = py_num(t.base, t.base_int ? PY_INT : NP_F64);
+  if (P.rbin & LSM_REWARD_SAFETY_VIOLATION) rew = py_add(rew, sv);
+  if (P.rbin & LSM_REWARD_POTENTIAL_CONFLICT)
+    rew = py_add(rew, me_cnt > 1 ? py_num(-1.0 * st * me, NP_F64) : py_num(0.0, PY_INT));
+  if ((P.rbin & LSM_REWARD_DIFF_FROM_FILTERED_ACTION) && P.use_filter_arg)   // reward_diff_from_filtered_action
+    rew = py_add(rew, S.dpre[i] ? py_num(0.0, PY_INT) : py_num(-1.0 * st * S.adiff[i], NP_F64));
+  if (P.rbin & LSM_REWARD_HJ_VALUE) rew = py_add(rew, hj);
+  // np.clip(rew, -40, 50): a Python int becomes np.int64; float32 stays float32 (bounds exact)
+  t.rew = np_clip(rew.v, -40.0, 50.0);
+  const size_t k = (size_t)env * N + i;
+  if (!P.collab) gptr(P.o.rew)[k] = (float)t.rew;
+  S.raw[i] = t.rew;
+  S.safe[i] = (double)(rew.t == PY_INT ? NP_I64 : rew.t);
+}
+
+// The shared reward (environment.py:1031-1037): np.sum(reward_n) -- the array's dtype is the
+// promotion of the agents' scalars, summed pairwise in it -- for every agent. After reward_finish
+// of all the env's agents.
+template <int NT>
+__device__ __forceinline__ void reward_shared(const KParams& P, const Lds& S, int env, int i) {
+  constexpr int DYN = 0;
+  LSM_DIMS;
+  bool f64 = false, f32 = false, i64 = false;
+  for (int j = 0; j < N; ++j) {
+    const int ty = (int)S.safe[j];
+    f64 |= ty == NP_F64;
+    f32 |= ty == NP_F32;
+    i64 |= ty == NP_I64;
+  }
+  double sum;
+  if (f32 && !f64 && !i64) {   // float32 pairwise sum (FLOAT_pairwise_sum)
+    if (N < 8) {
+      float r = 0.0f;
+      for (int j = 0; j < N; ++j) r += (float)S.raw[j];
+      sum = r;
+    } else {
+      float r[8];
+      for (int q = 0; q < 8; ++q) r[q] = (float)S.raw[q];
+      int j = 8;
+      for (; j < N - (N % 8); j += 8)
+        for (int q = 0; q < 8; ++q) r[q] += (float)S.raw[j + q];
+      float res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+      for (; j < N; ++j) res += (float)S.raw[j];
+      sum = res;
+    }
+  } else {   // float64 (int64 sums are exact in it)
+    sum = np_sum_rolled(S.raw, N);
+  }
+  gptr(P.o.rew)[(size_t)env * N + i] = (float)sum;
 }
 
 // info_callback accumulators of agent i (navigation_graph_safe.py:386-450); `ncoll` = other
@@ -2787,7 +3000,7 @@ __global__ __launch_bounds__(64, DYN == 0 ? (LPE == 64 ? 4 : 2) : LSM_WAVES_PER_
   // times on the same raw actions; the distances and min relative distance of the final state follow
   for (int it = 0; it < P.nis; ++it) {
   if (filter_on) {
-    const SepChain sc = sep_chain(S.sep);
+    const SepChain sc = sep_chain(S.sep, P.s, env);
     const int npairs = N * N;
     for (int p = lane; p < npairs; p += LPE) {
       const int j = p / N, i = p - j * N;   // [j][i]: ego i fastest (bank-conflict-free reads)
@@ -2846,8 +3059,13 @@ __global__ __launch_bounds__(64, DYN == 0 ? (LPE == 64 ? 4 : 2) : LSM_WAVES_PER_
   if (DYN == 0 && !P.use_filter_arg) mag = magnetic_penalty_wave<LPE, NT>(P, S, S.dpair);
   AgentTmp at;
   if (lane < N) reward_agent<DYN, NT>(P, S, env, lane, mag, at);
-  const double rew = at.rew;
   __syncthreads();
+  if (P.rext) {   // optional reward terms / shared reward: after every agent's goal / done update
+    if (lane < N) reward_finish<DYN, NT>(P, S, env, lane, at);
+    __syncthreads();
+    if (P.collab && lane < N) reward_shared<NT>(P, S, env, lane);
+  }
+  const double rew = at.rew;
   if (lane < N) S.emask[lane] = ego_mask(S, N, L, lane);
   if (S.dep0) {
     // graph_observation masks cached_dist_mag IN PLACE (navigation_graph_safe.py:986-987), so
@@ -2908,6 +3126,7 @@ __global__ __launch_bounds__(64, DYN == 0 ? (LPE == 64 ? 4 : 2) : LSM_WAVES_PER_
 #include "lsm_block.h"
 #include "lsm_team.h"
 
+#if LSM_HOST_PART
 // A new value table (a new HjDataHandle): every env's separation chain starts empty.
 __global__ void sep_clear_kernel(float4* rec, uint32_t rec_stride16, int n_envs, uint32_t sep_off) {
   const int env = blockIdx.x * blockDim.x + threadIdx.x;
@@ -2916,7 +3135,9 @@ __global__ void sep_clear_kernel(float4* rec, uint32_t rec_stride16, int n_envs,
   sep[0] = 0.0;
   sep[1] = 0.0;
 }
+#endif
 
+#if LSM_HOST_PART
 // env k's MT19937: np.random.seed(seed + 1000 * (env_offset + k))
 __global__ void seed_kernel(uint32_t* mt, int n_envs, int64_t seed, int64_t env_offset) {
   const int env = blockIdx.x * blockDim.x + threadIdx.x;
@@ -2926,6 +3147,7 @@ __global__ void seed_kernel(uint32_t* mt, int n_envs, int64_t seed, int64_t env_
   mt_seed(s, key, 1);
   key[MT_N] = MT_N;
 }
+#endif
 
 }  // namespace lsm
 
@@ -2976,6 +3198,11 @@ static int fail(lsm_env* e, const std::string& msg) {
   return 1;
 }
 
+// the reference builds an HjDataHandle (use_hj_handle, navigation_graph_safe.py:195)
+static bool uses_hj(const lsm_env* e) {
+  return e->cfg.use_safety_filter || (e->cfg.reward_terms & LSM_REWARD_HJ_VALUE);
+}
+
 #define HIPCHK(env, expr)                                                              \
   do {                                                                                 \
     hipError_t _e = (expr);                                                            \
@@ -2991,6 +3218,87 @@ static int dalloc(lsm_env* e, T** p, size_t count) {
   *p = (T*)q;
   return 0;
 }
+
+static const KParams* active_params(const lsm_env* e) {
+  return e->ring_sel >= 0 ? (const KParams*)(e->dring + e->ring_sel) : (const KParams*)e->dparams;
+}
+
+template <int DYN, int LPE, int NT>
+void launch_t(lsm_env* e, const KStep& L, size_t env_lds, hipStream_t st) {
+  constexpr int G = WAVE / LPE;
+  const int blocks = (e->cfg.num_envs + G - 1) / G;
+  hipLaunchKernelGGL((rollout_kernel<DYN, LPE, NT>), dim3(blocks), dim3(WAVE), env_lds * G, st,
+                     active_params(e), L);
+}
+
+template <int DYN, int NT, int G>
+int launch_team_t(lsm_env* e, const KStep& L, size_t env_bytes, hipStream_t st) {
+  static bool attr = false;   // LDS above the 64 KB default needs an explicit opt-in
+  const size_t lds = env_bytes * G;
+  if (!attr && lds > 65536) {
+    HIPCHK(e, hipFuncSetAttribute((const void*)rollout_team_kernel<DYN, NT, G>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    attr = true;
+  }
+  const int blocks = (e->cfg.num_envs + G - 1) / G;
+  hipLaunchKernelGGL((rollout_team_kernel<DYN, NT, G>), dim3(blocks), dim3(WAVE * G), lds, st,
+                     active_params(e), L);
+  return 0;
+}
+
+template <int DYN, int NT, bool NIS1>
+int launch_block_nis(lsm_env* e, const KStep& L, size_t env_lds, hipStream_t st) {
+  static bool attr = false;   // LDS above the 64 KB default needs an explicit opt-in
+  if (!attr && env_lds > 65536) {
+    HIPCHK(e, hipFuncSetAttribute((const void*)rollout_block_kernel<DYN, NT, NIS1>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)env_lds));
+    attr = true;
+  }
+  hipLaunchKernelGGL((rollout_block_kernel<DYN, NT, NIS1>), dim3(e->cfg.num_envs), dim3(BT), env_lds, st,
+                     active_params(e), L);
+  return 0;
+}
+
+template <int DYN, int NT>
+int launch_block_t(lsm_env* e, const KStep& L, size_t env_lds, hipStream_t st) {
+  return e->cfg.num_internal_step > 1 ? launch_block_nis<DYN, NT, false>(e, L, env_lds, st)
+                                      : launch_block_nis<DYN, NT, true>(e, L, env_lds, st);
+}
+
+
+// ---- kernel groups ------------------------------------------------------------------------
+// lsm.build compiles this file once per group (-DLSM_PART=g, in parallel) plus once for the host
+// code (-DLSM_PART=0, which declares every group's launchers extern); without LSM_PART everything
+// is one translation unit (diagnostic builds).
+#define LSM_G1(X) X(0, 64, 0) X(0, 32, 0) X(0, 16, 0) X(0, 32, 8) X(0, 64, 3) X(0, 64, 8)
+#define LSM_G2(X) X(1, 64, 0) X(1, 32, 0) X(1, 16, 0) X(1, 32, 16) X(1, 64, 3) X(1, 64, 16)
+#define LSM_G3(X) X(0, 8, 8) X(0, 8, 4) X(0, 8, 2)
+#define LSM_G4(X) X(1, 16, 4) X(1, 16, 2)
+#define LSM_G5(X) X(0, 64) X(0, 0)
+#define LSM_G6(X) X(1, 64) X(1, 0)
+#define LSM_RT(a, b, c) template void launch_t<a, b, c>(lsm_env*, const KStep&, size_t, hipStream_t);
+#define LSM_TT(a, b, c) template int launch_team_t<a, b, c>(lsm_env*, const KStep&, size_t, hipStream_t);
+#define LSM_BK(a, b) template int launch_block_t<a, b>(lsm_env*, const KStep&, size_t, hipStream_t);
+#define LSM_RT_E(a, b, c) extern LSM_RT(a, b, c)
+#define LSM_TT_E(a, b, c) extern LSM_TT(a, b, c)
+#define LSM_BK_E(a, b) extern LSM_BK(a, b)
+#if defined(LSM_PART) && LSM_PART == 0
+LSM_G1(LSM_RT_E) LSM_G2(LSM_RT_E) LSM_G3(LSM_TT_E) LSM_G4(LSM_TT_E) LSM_G5(LSM_BK_E) LSM_G6(LSM_BK_E)
+#elif defined(LSM_PART) && LSM_PART == 1
+LSM_G1(LSM_RT)
+#elif defined(LSM_PART) && LSM_PART == 2
+LSM_G2(LSM_RT)
+#elif defined(LSM_PART) && LSM_PART == 3
+LSM_G3(LSM_TT)
+#elif defined(LSM_PART) && LSM_PART == 4
+LSM_G4(LSM_TT)
+#elif defined(LSM_PART) && LSM_PART == 5
+LSM_G5(LSM_BK)
+#elif defined(LSM_PART) && LSM_PART == 6
+LSM_G6(LSM_BK)
+#endif
+
+#if LSM_HOST_PART
 
 static void fill_params(const lsm_env* e, KParams& P) {
   memset(&P, 0, sizeof(P));
@@ -3008,6 +3316,12 @@ static void fill_params(const lsm_env* e, KParams& P) {
   P.scenario = e->cfg.scenario;
   P.rng = e->cfg.rng;
   P.nis = e->cfg.num_internal_step > 1 ? e->cfg.num_internal_step : 1;
+  P.rbin = e->cfg.reward_terms;
+  P.collab = e->cfg.collaborative ? 1 : 0;
+  P.rext = (P.rbin != 0 || P.collab) ? 1 : 0;
+  P.use_hj = (e->cfg.use_safety_filter || (e->cfg.reward_terms & LSM_REWARD_HJ_VALUE)) ? 1 : 0;
+  P.mt_stage = 2 * MT_N;
+  if (const char* v = getenv("LSM_MT_STAGE")) P.mt_stage = std::max(1, std::min(2 * MT_N, atoi(v)));
   P.seed = e->cfg.seed;
   P.env_offset = e->cfg.env_offset;
   P.lds_dep_off = (uint32_t)lds_plan(e->N, e->NL, e->E, e->F, e->block).bytes;
@@ -3167,6 +3481,10 @@ int lsm_create(const lsm_config* cfg, lsm_env** out) {
   if (cfg->num_internal_step < 0 || cfg->num_internal_step > 64)
     return fail(e, "num_internal_step must be in [0, 64] (0 and 1: one inner step)");
   if (cfg->episode_length < 1) return fail(e, "episode_length must be >= 1");
+  if (cfg->reward_terms & ~LSM_REWARD_ALL)
+    return fail(e, "reward_terms: unknown LSM_REWARD_* bits (RewardBinaryConfig has four optional terms, "
+                   "multiagent/config.py:78-83)");
+  if (cfg->collaborative != 0 && cfg->collaborative != 1) return fail(e, "collaborative must be 0 or 1");
   e->N = N; e->L = L; e->NL = N * L; e->E = N * (1 + L);
   e->F = cfg->dynamics == LSM_DOUBLE_INTEGRATOR ? 10 : 11;
   e->OBS = cfg->dynamics == LSM_DOUBLE_INTEGRATOR ? 7 : 6;
@@ -3219,6 +3537,8 @@ int lsm_create(const lsm_config* cfg, lsm_env** out) {
   r |= dalloc(e, &e->pairs, (size_t)e->E * (e->E - 1) / 2 + 1);
   r |= dalloc(e, &e->action_err, 1);
   e->s.dep = nullptr;
+  e->s.sepx = nullptr;
+  e->s.sepx_cap = 0;
   if (cfg->scenario == LSM_SCENARIO_DEPARTURES) r |= dalloc(e, &e->s.dep, n * depw(N));
   if (r) return 1;
   if (e->s.dep) {   // Agent.departed defaults to True (core.py:343), timers 0
@@ -3270,7 +3590,7 @@ int lsm_create(const lsm_config* cfg, lsm_env** out) {
                      cfg->env_offset);
   HIPCHK(e, hipGetLastError());
   HIPCHK(e, hipDeviceSynchronize());
-  if (!cfg->use_safety_filter && cfg->dynamics == LSM_DOUBLE_INTEGRATOR) e->tables_ok = true;
+  e->tables_ok = !uses_hj(e) && cfg->dynamics == LSM_DOUBLE_INTEGRATOR;
   return 0;
 }
 
@@ -3398,7 +3718,7 @@ int lsm_set_ttr_table(lsm_env* e, int32_t ndim, const double* lo, const double* 
   if (ndim != 4) return fail(e, "TTR table must be 4-D");
   if (upload_table(e, e->ttr, ndim, lo, hi, shape, periodic, values, nullptr)) return 1;
   e->ttr_max = ttr_max;
-  e->tables_ok = !e->cfg.use_safety_filter || e->val.cells != nullptr;
+  e->tables_ok = !uses_hj(e) || e->val.cells != nullptr;
   e->params_dirty = true;
   return 0;
 }
@@ -3461,23 +3781,33 @@ static int check_ready(lsm_env* e, bool stepping) {
   return 0;
 }
 
-// Every env's shift chain holds at most KSEP entries; an env's chain grows only at its resets,
-// by one entry per change of the separation it resets with, so the changes across the calls'
-// curriculum blocks since the table upload bound every chain.
-static int sep_check(lsm_env* e, const lsm_curriculum* cur) {
-  if (!e->cfg.use_safety_filter) return 0;
-  if (cur->separation_distance != e->sep_last) {
-    if (e->sep_changes + 1 > KSEP)
-      return fail(e, "more than " + std::to_string(KSEP) + " separation-distance changes since the value table "
-                     "was set (per-env HJ shift chain is bounded); re-upload the table");
-    e->sep_changes++;
-    e->sep_last = cur->separation_distance;
+// An env's shift chain grows only at its resets, by one entry per change of the separation it
+// resets with, so the changes across the calls' curriculum blocks since the table upload bound every
+// chain. The record holds KSEP shifts; before a launch that could write shift k >= KSEP the per-env
+// overflow rows (StateDev::sepx) are grown, stream-ordered, keeping the shifts already there. The
+// reference has no bound (HjDataHandle.update_separation_distance shifts the table in place,
+// safety_filter.py:170-174); neither has this.
+static int sep_check(lsm_env* e, const lsm_curriculum* cur, hipStream_t st) {
+  if (!uses_hj(e)) return 0;
+  if (cur->separation_distance == e->sep_last) return 0;
+  e->sep_changes++;
+  e->sep_last = cur->separation_distance;
+  const uint32_t need = e->sep_changes > KSEP ? (uint32_t)(e->sep_changes - KSEP) : 0;
+  if (need <= e->s.sepx_cap) return 0;
+  const uint32_t cap = std::max<uint32_t>(std::max<uint32_t>(2 * e->s.sepx_cap, 16), need);
+  const size_t n = (size_t)e->cfg.num_envs;
+  double* nx = nullptr;
+  if (dalloc(e, &nx, n * cap)) return 1;
+  if (e->s.sepx) {
+    HIPCHK(e, hipMemcpy2DAsync(nx, (size_t)cap * 8, e->s.sepx, (size_t)e->s.sepx_cap * 8, (size_t)e->s.sepx_cap * 8,
+                               n, hipMemcpyDeviceToDevice, st));
+    HIPCHK(e, hipStreamSynchronize(st));
+    dfree(e, e->s.sepx);
   }
+  e->s.sepx = nx;
+  e->s.sepx_cap = cap;
+  e->params_dirty = true;
   return 0;
-}
-
-static const KParams* active_params(const lsm_env* e) {
-  return e->ring_sel >= 0 ? (const KParams*)(e->dring + e->ring_sel) : (const KParams*)e->dparams;
 }
 
 // output pointers of ring index i (see lsm_env::ring_*)
@@ -3500,48 +3830,6 @@ static void apply_ring(const lsm_env* e, int i, KParams& P) {
   P.o.masks = (float*)at(LSM_OUT_MASKS, P.o.masks);
   P.o.active_masks = (float*)at(LSM_OUT_ACTIVE_MASKS, P.o.active_masks);
   P.o.cforce = (double*)at(LSM_OUT_COLLISION_FORCE, P.o.cforce);
-}
-
-extern "C++" template <int DYN, int LPE, int NT>
-static void launch_t(lsm_env* e, const KStep& L, size_t env_lds, hipStream_t st) {
-  constexpr int G = WAVE / LPE;
-  const int blocks = (e->cfg.num_envs + G - 1) / G;
-  hipLaunchKernelGGL((rollout_kernel<DYN, LPE, NT>), dim3(blocks), dim3(WAVE), env_lds * G, st,
-                     active_params(e), L);
-}
-
-extern "C++" template <int DYN, int NT, int G>
-static int launch_team_t(lsm_env* e, const KStep& L, size_t env_bytes, hipStream_t st) {
-  static bool attr = false;   // LDS above the 64 KB default needs an explicit opt-in
-  const size_t lds = env_bytes * G;
-  if (!attr && lds > 65536) {
-    HIPCHK(e, hipFuncSetAttribute((const void*)rollout_team_kernel<DYN, NT, G>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    attr = true;
-  }
-  const int blocks = (e->cfg.num_envs + G - 1) / G;
-  hipLaunchKernelGGL((rollout_team_kernel<DYN, NT, G>), dim3(blocks), dim3(WAVE * G), lds, st,
-                     active_params(e), L);
-  return 0;
-}
-
-extern "C++" template <int DYN, int NT, bool NIS1>
-static int launch_block_nis(lsm_env* e, const KStep& L, size_t env_lds, hipStream_t st) {
-  static bool attr = false;   // LDS above the 64 KB default needs an explicit opt-in
-  if (!attr && env_lds > 65536) {
-    HIPCHK(e, hipFuncSetAttribute((const void*)rollout_block_kernel<DYN, NT, NIS1>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)env_lds));
-    attr = true;
-  }
-  hipLaunchKernelGGL((rollout_block_kernel<DYN, NT, NIS1>), dim3(e->cfg.num_envs), dim3(BT), env_lds, st,
-                     active_params(e), L);
-  return 0;
-}
-
-extern "C++" template <int DYN, int NT>
-static int launch_block_t(lsm_env* e, const KStep& L, size_t env_lds, hipStream_t st) {
-  return e->cfg.num_internal_step > 1 ? launch_block_nis<DYN, NT, false>(e, L, env_lds, st)
-                                      : launch_block_nis<DYN, NT, true>(e, L, env_lds, st);
 }
 
 static int launch(lsm_env* e, KStep& L, hipStream_t st) {
@@ -3672,7 +3960,7 @@ int lsm_reset(lsm_env* e, const lsm_curriculum* cur, void* stream) {
   if (!e || !cur) return 1;
   if (e->cfg.scenario != LSM_SCENARIO_TRAIN) return fail(e, "layout scenario: reset with lsm_reset_layout");
   if (check_ready(e, false)) return 1;
-  if (sep_check(e, cur)) return 1;
+  if (sep_check(e, cur, (hipStream_t)stream)) return 1;
   KStep L;
   memset(&L, 0, sizeof(L));
   memcpy(L.cur_new, cur, sizeof(double) * NCUR);
@@ -3686,7 +3974,7 @@ int lsm_reset_layout(lsm_env* e, const lsm_curriculum* cur, const double* layout
   if (e->cfg.scenario == LSM_SCENARIO_TRAIN) return fail(e, "lsm_reset_layout needs a layout scenario");
   if (!layout) return fail(e, "null layout");
   if (check_ready(e, false)) return 1;
-  if (sep_check(e, cur)) return 1;
+  if (sep_check(e, cur, (hipStream_t)stream)) return 1;
   KStep L;
   memset(&L, 0, sizeof(L));
   memcpy(L.cur_new, cur, sizeof(double) * NCUR);
@@ -3700,7 +3988,7 @@ int lsm_step(lsm_env* e, const void* actions, int32_t kind, const lsm_curriculum
   if (kind < 0 || kind > 2) return fail(e, "bad action kind");
   if (check_ready(e, true)) return 1;
   // a step's curriculum block is used only by its auto-resets: without them no chain can grow
-  if (e->cfg.auto_reset && sep_check(e, cur)) return 1;
+  if (e->cfg.auto_reset && sep_check(e, cur, (hipStream_t)stream)) return 1;
   KStep L;
   memset(&L, 0, sizeof(L));
   memcpy(L.cur_new, cur, sizeof(double) * NCUR);
@@ -3779,3 +4067,5 @@ int lsm_host_scenario(const lsm_config* cfg, const lsm_curriculum* cur, uint32_t
 }
 
 }  // extern "C"
+
+#endif  // LSM_HOST_PART

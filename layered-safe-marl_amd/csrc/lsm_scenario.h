@@ -42,6 +42,7 @@ LSM_HD void separated_positions(Rng& rng, int n, double x0, double x1, double y0
           if (k == 0 || dk < d) d = dk;
         }
         if (d > dmin && d < dmax) break;
+        if (rng.exhausted()) break;   // a lane stream ran out: the scenario is redrawn (lsm_team.h)
       }
     } else {
       x = rng.uniform(x0, x1);

@@ -79,21 +79,25 @@ __device__ __forceinline__ void mt_next_block(const uint32_t* key, uint32_t* nxt
 
 // One env's numpy stream for a lane that draws that env's scenario alone: the current block
 // from pos on, then the next block. A scenario needing more (over 624 words beyond the current
-// block) sets `over`; the env's wave then redraws it with the cooperative stream.
+// block, or past `lim`: KParams::mt_stage, LSM_MT_STAGE, which tests lower to exercise this path)
+// sets `over` and stops the draw (the rejection loops check exhausted()); the env's wave then
+// redraws it with the cooperative stream.
 constexpr uint32_t MT_OVER = 0xffffffffu;
 struct LaneMT {
   const uint32_t* key;
   const uint32_t* nxt;
   int pos;
+  int lim;   // first position not served (<= 2 MT_N)
   bool over;
   __device__ __forceinline__ uint32_t next32() {
     uint32_t y = 0;
-    if (pos < MT_N) y = key[pos];
-    else if (pos < 2 * MT_N) y = nxt[pos - MT_N];
-    else over = true;
+    if (pos >= lim) over = true;
+    else if (pos < MT_N) y = key[pos];
+    else y = nxt[pos - MT_N];
     ++pos;
     return mt_temper(y);
   }
+  __device__ __forceinline__ bool exhausted() const { return over; }
   __device__ __forceinline__ double next_double() {
     const uint32_t a = next32() >> 5, b = next32() >> 6;
     return (a * 67108864.0 + b) / 9007199254740992.0;
@@ -137,6 +141,7 @@ __device__ __forceinline__ void team_scenario(const KParams& P, unsigned char* s
   rng.key = S.mt;
   rng.nxt = S.mtn;
   rng.pos = (int)S.mt[MT_N];
+  rng.lim = min(2 * MT_N, rng.pos + P.mt_stage);
   rng.over = false;
   random_scenario(rng, sp, S.ps, S.lm, S.scen);
   S.mt[MT_N] = rng.over ? MT_OVER : (uint32_t)rng.pos;
@@ -268,7 +273,7 @@ void rollout_team_kernel(const KParams* __restrict__ Pp, const KStep K) {
     if (lane < N) decode_action(P, S, N, lane, act);
     filter_on = S.cur[C_FILT] != 0.0;
     if (filter_on) {
-      const SepChain sc = sep_chain(S.sep);
+      const SepChain sc = sep_chain(S.sep, P.s, env);
       for (int p = lane; p < N * N; p += LPE) {
         const int j = p / N, i = p - j * N;   // [j][i]: ego i fastest (bank-conflict-free reads)
         if (i == j || S.dpre[i] || S.dpre[j]) continue;
@@ -359,6 +364,11 @@ void rollout_team_kernel(const KParams* __restrict__ Pp, const KStep K) {
       reward_agent<DYN, NT>(P, A, aenv, ai, mag, at);
     }
     esync<LPE>();   // every agent's goal / done update before the snapshot masks
+    if (P.rext) {   // optional reward terms / shared reward (reward_finish)
+      if (alane) reward_finish<DYN, NT>(P, A, aenv, ai, at);
+      esync<LPE>();
+      if (P.collab && alane) reward_shared<NT>(P, A, aenv, ai);
+    }
     TSTAMP(10);
     const int acstep = A.step[0] + 1;
     if (alane) {

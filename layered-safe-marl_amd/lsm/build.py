@@ -1,6 +1,10 @@
 """Build ``liblsm_rollout.so`` in-tree with hipcc for gfx950 (no JIT cache, no CMake).
 
 ``python -m lsm.build`` (from ``layered-safe-marl_amd/``) or ``__graft_entry__.build()``.
+
+The rollout translation unit instantiates ~25 kernels; it is compiled as ``ROLLOUT_PARTS``
+objects in parallel (``-DLSM_PART=0`` the host code, ``-DLSM_PART=g`` kernel group g, see the
+group table in ``csrc/lsm_rollout.hip``) and linked with the other units.
 """
 from __future__ import annotations
 
@@ -10,12 +14,13 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(os.path.dirname(HERE), "csrc")
-SRC = os.path.join(CSRC, "lsm_rollout.hip")   # the rollout TU (diagnostic builds recompile it alone)
+SRC = os.path.join(CSRC, "lsm_rollout.hip")   # the rollout TU
 OUT = os.path.join(CSRC, "liblsm_rollout.so")
 HDR = os.path.join(os.path.dirname(os.path.dirname(HERE)), "include", "lsm_rollout.h")
-# translation units -> their dependencies (each compiled to its own object, then linked)
+ROLLOUT_DEPS = ["lsm_numeric.h", "lsm_scenario.h", "lsm_block.h", "lsm_rk45.h", "lsm_pow_tables.h", "lsm_team.h"]
+ROLLOUT_PARTS = 7
+# the other translation units -> their dependencies (each compiled to its own object, then linked)
 UNITS = {
-    "lsm_rollout.hip": ["lsm_numeric.h", "lsm_scenario.h", "lsm_block.h", "lsm_rk45.h", "lsm_pow_tables.h", "lsm_team.h"],
     "lsm_edges.hip": [],
     "lsm_buffer.hip": [],
     "lsm_metrics.hip": [],
@@ -25,7 +30,10 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC",
          # reproduce numpy's float64 expression order exactly; explicit fma() only where
          # OpenBLAS fuses (lsm_numeric.h)
-         "-ffp-contract=off", "-Wno-unused-result"]
+         "-ffp-contract=off", "-Wno-unused-result", "-Wno-unused-function"]
+# Variant / diagnostic builds define this; csrc/lsm_rollout.hip refuses its diagnostic switches
+# (LSM_XP_*: bounds with wrong results, LSM_STAMPS) without it, so the product build cannot get one.
+DIAG_DEFINE = "LSM_DIAGNOSTIC_BUILD"
 
 
 def _stale(target: str, deps) -> bool:
@@ -39,73 +47,101 @@ def _obj(unit: str) -> str:
     return os.path.join(CSRC, unit.rsplit(".", 1)[0] + ".o")
 
 
+def _part_obj(part: int, tag: str = "") -> str:
+    return os.path.join(CSRC, "lsm_rollout%s_p%d.o" % (tag, part))
+
+
+def _rollout_deps():
+    return [SRC, HDR] + [os.path.join(CSRC, d) for d in ROLLOUT_DEPS]
+
+
+def _run_parallel(jobs, verbose=True):
+    """jobs: [(cmd, out)] -- each compiles into out + '.tmp', renamed on success."""
+    limit = max(1, min(len(jobs), int(os.environ.get("MAX_JOBS", os.cpu_count() or 4))))
+    pending = list(jobs)
+    running = []
+    failed = []
+    while pending or running:
+        while pending and len(running) < limit:
+            cmd, out = pending.pop(0)
+            if verbose:
+                print(" ".join(cmd), flush=True)
+            running.append((subprocess.Popen(cmd, cwd=CSRC), out))
+        p, out = running.pop(0)
+        if p.wait() != 0:
+            failed.append(out)
+        elif os.path.exists(out + ".tmp"):
+            os.replace(out + ".tmp", out)
+    if failed:
+        raise RuntimeError("compile failed: %s" % ", ".join(os.path.basename(f) for f in failed))
+
+
+def _rollout_jobs(defines=(), tag="", force=True):
+    jobs = []
+    for part in range(ROLLOUT_PARTS):
+        o = _part_obj(part, tag)
+        if force or _stale(o, _rollout_deps()):
+            cmd = [HIPCC] + FLAGS + ["-D%s" % d for d in defines] + ["-DLSM_PART=%d" % part, "-c", "-o", o + ".tmp",
+                                                                   "lsm_rollout.hip"]
+            jobs.append((cmd, o))
+    return jobs
+
+
 def needs_build() -> bool:
-    objs = [_obj(u) for u in UNITS]
-    return _stale(OUT, objs) or any(
+    objs = [_obj(u) for u in UNITS] + [_part_obj(p) for p in range(ROLLOUT_PARTS)]
+    return _stale(OUT, objs) or any(_stale(_part_obj(p), _rollout_deps()) for p in range(ROLLOUT_PARTS)) or any(
         _stale(_obj(u), [os.path.join(CSRC, u), HDR] + [os.path.join(CSRC, d) for d in deps])
         for u, deps in UNITS.items())
+
+
+def _link(objs, out, verbose=True):
+    cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", out + ".tmp"] + objs
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.check_call(cmd, cwd=CSRC)
+    os.replace(out + ".tmp", out)
 
 
 def build(force: bool = False, verbose: bool = True) -> str:
     if not force and not needs_build():
         return OUT
-    objs = []
+    jobs = _rollout_jobs(force=force)
     for u, deps in UNITS.items():
         o = _obj(u)
-        objs.append(o)
         if force or _stale(o, [os.path.join(CSRC, u), HDR] + [os.path.join(CSRC, d) for d in deps]):
-            cmd = [HIPCC] + FLAGS + ["-c", "-o", o + ".tmp", u]
-            if verbose:
-                print(" ".join(cmd), flush=True)
-            subprocess.check_call(cmd, cwd=CSRC)
-            os.replace(o + ".tmp", o)
-    cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", OUT + ".tmp"] + objs
-    if verbose:
-        print(" ".join(cmd), flush=True)
-    subprocess.check_call(cmd, cwd=CSRC)
-    os.replace(OUT + ".tmp", OUT)
+            jobs.append(([HIPCC] + FLAGS + ["-c", "-o", o + ".tmp", u], o))
+    _run_parallel(jobs, verbose)
+    _link([_part_obj(p) for p in range(ROLLOUT_PARTS)] + [_obj(u) for u in UNITS], OUT, verbose)
     return OUT
 
 
-def build_variant(name: str, defines, verbose: bool = True) -> str:
-    """A/B experiments: the rollout TU rebuilt with extra -D flags and linked with the product's
-    other objects into csrc/liblsm_rollout_<name>.so (select it with LSM_LIB=...). Never the
-    product library."""
-    build(verbose=verbose)
-    out = os.path.join(CSRC, "liblsm_rollout_%s.so" % name)
-    obj = out[:-3] + ".o"
-    cmd = [HIPCC] + FLAGS + ["-D%s" % d for d in defines] + ["-c", "-o", obj, "lsm_rollout.hip"]
-    if verbose:
-        print(" ".join(cmd), flush=True)
-    subprocess.check_call(cmd, cwd=CSRC)
-    objs = [obj] + [_obj(u) for u in UNITS if u != "lsm_rollout.hip"]
-    subprocess.check_call([HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", out] + objs, cwd=CSRC)
-    os.remove(obj)
-    return out
+def variant_path(name: str) -> str:
+    return os.path.join(CSRC, "liblsm_rollout_%s.so" % name)
 
 
 def build_variants(specs, verbose: bool = True):
-    """Several A/B variants at once: the product library and each variant's rollout object
-    compile in parallel (one hipcc process each), then each variant links. specs: NAME:D1,D2."""
-    import threading
-    t = threading.Thread(target=build, kwargs={"verbose": verbose})
-    t.start()
-    procs = []
+    """A/B experiments and diagnostic builds: the rollout TU rebuilt with extra -D flags and linked
+    with the product's other objects into csrc/liblsm_rollout_<name>.so (select it with LSM_LIB=...).
+    Never the product library. specs: ["NAME:D1,D2", ...]; all parts of all variants compile in
+    parallel."""
+    build(verbose=verbose)
+    jobs, variants = [], []
     for spec in specs:
         name, _, defs = spec.partition(":")
-        obj = os.path.join(CSRC, "liblsm_rollout_%s.o" % name)
-        cmd = [HIPCC] + FLAGS + ["-D%s" % d for d in filter(None, defs.split(","))] + ["-c", "-o", obj, "lsm_rollout.hip"]
-        if verbose:
-            print(" ".join(cmd), flush=True)
-        procs.append((name, obj, subprocess.Popen(cmd, cwd=CSRC, stderr=subprocess.DEVNULL)))
-    t.join()
-    for name, obj, pr in procs:
-        if pr.wait() != 0:
-            raise RuntimeError("variant %s failed to compile" % name)
-        out = os.path.join(CSRC, "liblsm_rollout_%s.so" % name)
-        objs = [obj] + [_obj(u) for u in UNITS if u != "lsm_rollout.hip"]
-        subprocess.check_call([HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", out] + objs, cwd=CSRC)
-        os.remove(obj)
+        defines = [d for d in defs.split(",") if d] + [DIAG_DEFINE]
+        jobs += _rollout_jobs(defines, tag="_" + name)
+        variants.append(name)
+    _run_parallel(jobs, verbose)
+    for name in variants:
+        parts = [_part_obj(p, "_" + name) for p in range(ROLLOUT_PARTS)]
+        _link(parts + [_obj(u) for u in UNITS], variant_path(name), verbose)
+        for o in parts:
+            os.remove(o)
+    return [variant_path(n) for n in variants]
+
+
+def build_variant(name: str, defines, verbose: bool = True) -> str:
+    return build_variants(["%s:%s" % (name, ",".join(defines))], verbose)[0]
 
 
 if __name__ == "__main__":

@@ -22,6 +22,8 @@ NUM_OUT = 17
 LSM_SCENARIO_TRAIN, LSM_SCENARIO_LAYOUT, LSM_SCENARIO_DEPARTURES = 0, 1, 2
 LSM_RNG_MT19937, LSM_RNG_PHILOX = 0, 1
 ADJ_REFERENCE, ADJ_COMPACT = 0, 1
+# lsm_config.reward_terms bits: RewardBinaryConfig's optional reward terms (multiagent/config.py:78-83)
+REWARD_BITS = {"safety_violation": 1, "potential_conflict": 2, "diff_from_filtered_action": 4, "hj_value": 8}
 INFO_FIELDS = ("individual_reward", "min_relative_distance", "Dist_to_goal", "Time_req_to_goal",
                "Num_agent_collisions", "Distance_mean", "Distance_variance", "Dists_traveled",
                "Time_mean", "Time_stddev", "Min_time_to_goal", "Safety filtered", "Safety violated",
@@ -45,14 +47,14 @@ class LsmConfig(C.Structure):
                 ("auto_reset", C.c_int32), ("emit_edges", C.c_int32), ("adj_layout", C.c_int32),
                 ("world_size", C.c_double), ("seed", C.c_int64), ("env_offset", C.c_int64),
                 ("collision_forces", C.c_int32), ("scenario", C.c_int32), ("rng", C.c_int32),
-                ("num_internal_step", C.c_int32)]
+                ("num_internal_step", C.c_int32), ("reward_terms", C.c_int32), ("collaborative", C.c_int32)]
 
 
 class LsmCurriculum(C.Structure):
     _fields_ = [(n, C.c_double) for n in (
         "curriculum_ratio", "sloped", "stair", "ratio_airtaxi", "ratio_scenario",
         "goal_heading_error_thresh", "goal_speed_error_thresh", "min_dist_thresh",
-        "separation_distance", "engagement_distance", "world_use_safety_filter", "reserved")]
+        "separation_distance", "engagement_distance", "world_use_safety_filter", "stair_is_int")]
 
 
 class LsmError(RuntimeError):
@@ -108,8 +110,8 @@ def load_library(path: str = LIB_PATH):
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name, None)
-        if fn is None and os.environ.get("LSM_LIB"):
-            continue   # an older library under A/B (tools/ab_bench.py) lacks a newer entry point
+        if fn is None and os.environ.get("LSM_LIB_AB") == "1":
+            continue   # tools/ab_bench.py --allow-old: an older library may lack a newer entry point
         if fn is None:
             raise AttributeError("%s: missing symbol %s" % (path, name))
         fn.restype = res

@@ -78,6 +78,13 @@ class RewardBinaryConfig:
     DIFF_FROM_FILTERED_ACTION = False
 
 
+REWARD_TERMS = {   # EnvArgs.reward_terms names -> RewardBinaryConfig switch (config.py:78-83)
+    "safety_violation": "SAFETY_VIOLATION",
+    "potential_conflict": "POTENTIAL_CONFLICT",
+    "diff_from_filtered_action": "DIFF_FROM_FILTERED_ACTION",
+    "hj_value": "HJ_VALUE",
+}
+
 ENTITY_SIZE = 0.050          # multiagent/core.py:261
 EPS_HJ = 0.4                 # multiagent/safety_filter.py:235,410
 
@@ -114,10 +121,24 @@ class EnvArgs:
     # RewardBinaryConfig.SEPARATION_DISTANCE_CURRICULUM (a hand-edited class constant in the
     # reference, config.py:81); None = that constant, True / False override it per env handle
     separation_distance_curriculum: Optional[bool] = None
+    # RewardBinaryConfig's optional reward terms (config.py:78-83, class constants the reference's
+    # users edit): None = those constants; else the names of the terms switched on, a subset of
+    # REWARD_TERMS (navigation_graph_safe.py:793-850)
+    reward_terms: Optional[tuple] = None
     # evaluation scenarios: multiagent.config.eval_scenario_type (a module constant in the
     # reference) and the Bay Area map's (width, height) in pixels (the image is not in the reference)
     eval_scenario_type: str = EVAL_SCENARIO_TYPE
     bayarea_image_size: Optional[tuple] = None
+
+    def active_reward_terms(self) -> tuple:
+        """The optional reward terms in effect (names, REWARD_TERMS order)."""
+        if self.reward_terms is None:
+            return tuple(k for k in REWARD_TERMS if getattr(RewardBinaryConfig, REWARD_TERMS[k]))
+        return tuple(k for k in REWARD_TERMS if k in self.reward_terms)
+
+    def uses_hj_handle(self) -> bool:
+        """use_hj_handle = use_safety_filter or RewardBinaryConfig.HJ_VALUE (navigation_graph_safe.py:195)."""
+        return bool(self.use_safety_filter) or "hj_value" in self.active_reward_terms()
 
     def sep_curriculum(self) -> bool:
         v = self.separation_distance_curriculum
@@ -154,6 +175,12 @@ class EnvArgs:
             raise ValueError("num_internal_step must be in [1, 64] (World.step's inner loop, core.py:607)")
         if not self.discrete_action:
             raise ValueError("only the Discrete(25) action space is on the path")
+        if self.reward_terms is not None:
+            bad = sorted(set(self.reward_terms) - set(REWARD_TERMS))
+            if bad:
+                raise ValueError("unknown reward_terms %s (RewardBinaryConfig has %s)" % (bad, sorted(REWARD_TERMS)))
+        if not isinstance(self.collaborative, (bool, int)) or int(self.collaborative) not in (0, 1):
+            raise ValueError("collaborative must be a bool (MultiAgentGraphEnv.shared_reward)")
         total = int(self.num_env_steps) // self.episode_length // self.n_rollout_threads
         if total == 0:
             raise ValueError("num_env_steps // episode_length // n_rollout_threads == 0: the "

@@ -55,7 +55,10 @@ def curriculum_block(args, num_current_episode: int) -> dict:
                 ratio_scenario=float(crs), goal_heading_error_thresh=float(ghe),
                 goal_speed_error_thresh=float(gse), min_dist_thresh=float(mdt),
                 separation_distance=float(sep), engagement_distance=float(eng),
-                world_use_safety_filter=1.0 if world_filter else 0.0, reserved=0.0)
+                world_use_safety_filter=1.0 if world_filter else 0.0,
+                # _stair returns the Python int 0 / 1 outside its ramp (:1115-1118): the scaled reward
+                # weights (:340-345) are then ints, which keeps reward_hj_value's products float32
+                stair_is_int=1.0 if isinstance(st, int) else 0.0)
 
 
 def to_struct(block: dict):

@@ -10,7 +10,6 @@ from __future__ import annotations
 
 import argparse
 import os
-import subprocess
 import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -22,11 +21,7 @@ PHASES = ["load", "decode", "filter-pairs", "filter-ego", "integrate", "dist+min
 
 def build_stamps():
     from . import build
-    cmd = [build.HIPCC] + build.FLAGS + ["-shared", "-DLSM_STAMPS", "-o", STAMP_LIB, build.SRC,
-                                        os.path.join(CSRC, "lsm_edges.hip"),
-                                        os.path.join(CSRC, "lsm_buffer.hip"),
-                                        os.path.join(CSRC, "lsm_metrics.hip")]
-    subprocess.check_call(cmd, cwd=CSRC)
+    build.build_variant("stamps", ["LSM_STAMPS"])
 
 
 def main():

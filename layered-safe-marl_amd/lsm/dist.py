@@ -26,6 +26,36 @@ def rank_info():
             int(os.environ.get("LOCAL_RANK", 0)))
 
 
+def init_rank(backend: str = "nccl", device_index=None):
+    """Bind this rank to its GPU, then join the process group: torch.cuda.set_device before
+    init_process_group, and (RCCL) the device passed as device_id, so the communicator and every
+    barrier of rank r use GPU r -- a communicator created before the device is set binds to GPU 0 on
+    every rank. Returns the rank's device (None without CUDA, e.g. gloo on the CPU)."""
+    import torch.distributed as dist
+    _, world, local_rank = rank_info()
+    dev = None
+    if torch.cuda.is_available():
+        dev = torch.device("cuda:%d" % (local_rank if device_index is None else device_index))
+        torch.cuda.set_device(dev)
+    if world > 1 and not dist.is_initialized():
+        if backend == "nccl":
+            dist.init_process_group(backend, device_id=dev)
+        else:
+            dist.init_process_group(backend)
+    return dev
+
+
+def barrier(backend: str = "nccl"):
+    """dist.barrier on this rank's own GPU (RCCL: device_ids = [the current device])."""
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()):
+        return
+    if backend == "nccl" and torch.cuda.is_available():
+        dist.barrier(device_ids=[torch.cuda.current_device()])
+    else:
+        dist.barrier()
+
+
 def shard(n_global: int, rank: int, world: int):
     """(env_offset, n_local) of a rank; the remainder goes to the first ranks."""
     base, rem = divmod(n_global, world)
@@ -61,8 +91,9 @@ class EpisodeSummaryReducer:
     def __init__(self, n_local: int, device, group=None):
         self.group = group
         self.device = torch.device(device)
-        # the env count rides in the SUM buffer (one collective gives sums and the global count)
-        self._cnt = torch.full((1,), float(n_local), dtype=torch.float64)
+        # the env count rides in the SUM buffer (one collective gives sums and the global count);
+        # it is the row count of each submitted ep_info (n_local for the rollout's LSM_OUT_EP_INFO)
+        self.n_local = int(n_local)
         self._pending = []
 
     def submit(self, ep_info: torch.Tensor):
@@ -72,6 +103,9 @@ class EpisodeSummaryReducer:
             import ctypes as C
             from . import capi
             lib = capi.load_library()
+            if getattr(lib, "lsm_episode_summary", None) is None:
+                raise capi.LsmError("%s lacks lsm_episode_summary (a library older than lsm_metrics.hip)"
+                                    % capi.LIB_PATH)
             ep = ep_info.contiguous()
             st = torch.cuda.current_stream(ep.device).cuda_stream
             if lib.lsm_episode_summary(C.c_void_p(ep.data_ptr()), int(ep.shape[0]), C.c_void_p(out.data_ptr()),
@@ -79,7 +113,7 @@ class EpisodeSummaryReducer:
                 raise capi.LsmError("lsm_episode_summary failed")
         else:   # host tensors (gloo tests on the CPU): the same sums with torch
             torch.sum(ep_info, dim=0, out=out[:8])
-            out[8:9].copy_(self._cnt.to(out.device))
+            out[8] = float(ep_info.shape[0])   # the rows submitted, as the device path counts them
             out[9:10] = torch.amin(ep_info[:, 6:7], dim=0)
         buf, mn = out[:9], out[9:10]
         works = ()

@@ -150,19 +150,23 @@ class GpuGraphVecEnv(ShareVecEnv):
                              collision_forces=int(bool(collision_forces)),
                              scenario=layout.scenario_code if layout is not None else capi.LSM_SCENARIO_TRAIN,
                              rng=capi.LSM_RNG_PHILOX if rng == "philox" else capi.LSM_RNG_MT19937,
-                             num_internal_step=int(a.num_internal_step))
+                             num_internal_step=int(a.num_internal_step),
+                             reward_terms=sum(capi.REWARD_BITS[k] for k in a.active_reward_terms()),
+                             collaborative=int(bool(a.collaborative)))
+        self.collaborative = bool(a.collaborative)
         if int(a.seed) + 1000 * (int(env_offset) + self.num_envs - 1) >= 2 ** 32:
             raise ValueError("numpy seeds must be < 2**32 (seed + 1000 * env index)")
         h = C.c_void_p()
         rc = self.lib.lsm_create(C.byref(cfg), C.byref(h))
         self.h = h
         capi.check(rc, h)
-        # HJ / TTR tables (synthetic stand-ins for the absent pickles unless given)
-        if a.use_safety_filter or not di:
+        # HJ / TTR tables (synthetic stand-ins for the absent pickles unless given); the HJ handle exists
+        # with the filter on or RewardBinaryConfig.HJ_VALUE (navigation_graph_safe.py:195)
+        if a.uses_hj_handle() or not di:
             vt, tt = default_tables(a.dynamics_type, small=small_tables, target_separation=a.initial_separation())
             value_table = value_table if value_table is not None else vt
             ttr_table = ttr_table if ttr_table is not None else tt
-        self.value_table = value_table if a.use_safety_filter else None
+        self.value_table = value_table if a.uses_hj_handle() else None
         self.ttr_table = ttr_table if not di else None
         if self.value_table is not None:
             self._upload_value_table()
@@ -317,15 +321,18 @@ class GpuGraphVecEnv(ShareVecEnv):
 
     def step_wait(self):
         self._pending = None
+        # shared reward (collaborative): each worker returns [[sum]] * N, stacked (n, N, 1)
+        # (environment.py:1031-1037, env_wrappers.py:988-996); else (n, N)
+        t_rew = self.t_rew.unsqueeze(-1) if self.collaborative else self.t_rew
         if not self.return_numpy:
-            out = (self.t_obs, self.agent_id, self.t_node, self.t_adj, self.t_rew, self.t_done,
+            out = (self.t_obs, self.agent_id, self.t_node, self.t_adj, t_rew, self.t_done,
                    (self.t_info, self.t_reset, self.t_epinfo))
             return out + (0,) if not self.auto_reset else out
         self.check_actions()   # the host copies below synchronise anyway
         obs = self._host64(self.t_obs)
         node = self._host64(self.t_node)
         adj = self._host64(self.reference_adj())
-        rew = self._host64(self.t_rew)
+        rew = self._host64(t_rew)
         dones = self.t_done.cpu().numpy().astype(bool)
         infos = self._infos() if self.build_infos else None
         aid = self.agent_id.cpu().numpy()

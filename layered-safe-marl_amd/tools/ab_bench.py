@@ -38,14 +38,19 @@ def main():
     ap.add_argument("--steps", type=int, default=500)
     ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--allow-old", action="store_true",
+                    help="libraries older than the Python side may lack newer entry points (LSM_LIB_AB=1)")
+    ap.add_argument("--bench-args", default="", help="extra bench.py arguments (e.g. '--steps 20')")
     a = ap.parse_args()
     vs = [parse(v) for v in a.variants]
     res = {n: [] for n, _ in vs}
     for _ in range(a.reps):
         for name, extra in vs:
             env = dict(os.environ, **extra)
+            if a.allow_old:
+                env["LSM_LIB_AB"] = "1"
             cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--config", str(a.config), "--steps",
-                   str(a.steps), "--warmup", str(a.warmup), "--no-cpu-baseline"]
+                   str(a.steps), "--warmup", str(a.warmup), "--no-cpu-baseline"] + a.bench_args.split()
             out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
             if out.returncode != 0:
                 print(name, "FAILED", out.stderr[-2000:], flush=True)

@@ -80,6 +80,10 @@ class _DI:
 
 GOAL_REACH = 50
 MIN_REWARD, MAX_REWARD = -40, 50
+# RewardWeightConfig (multiagent/config.py:64-73)
+RW_SAFETY_VIOLATION, RW_HJ_VALUE, RW_POTENTIAL_CONFLICT, RW_DIFF_FROM_FILTERED_ACTION = -20, -2, -1, -1
+# RewardBinaryConfig switches of the optional reward terms (config.py:78-83), by name
+REWARD_TERMS = ("safety_violation", "potential_conflict", "diff_from_filtered_action", "hj_value")
 SIZE = 0.050
 
 
@@ -177,6 +181,25 @@ class OracleEnv:
         self.num_total_episode = int(g("num_env_steps")) // self.episode_length // int(g("n_rollout_threads"))
         self.use_safety_filter = bool(g("use_safety_filter"))
         self.use_masking = bool(g("use_masking", True))
+        # RewardBinaryConfig's optional reward terms (multiagent/config.py:75-83, all False there;
+        # read in SafeAamScenario.reward, navigation_graph_safe.py:843-850) and the shared reward of
+        # MultiAgentGraphEnv (shared_reward = world.collaborative, environment.py:79-80,1031-1037)
+        terms = tuple(g("reward_terms") or ())
+        bad = set(terms) - set(REWARD_TERMS)
+        if bad:
+            raise ValueError("unknown reward terms %s" % sorted(bad))
+        self.rw_safety_violation = "safety_violation" in terms
+        self.rw_potential_conflict = "potential_conflict" in terms
+        self.rw_diff_from_filtered_action = "diff_from_filtered_action" in terms
+        self.rw_hj_value = "hj_value" in terms
+        self.collaborative = bool(g("collaborative", False))
+        # use_hj_handle = use_safety_filter or RewardBinaryConfig.HJ_VALUE (navigation_graph_safe.py:195)
+        self.use_hj = self.use_safety_filter or self.rw_hj_value
+        # update_curriculum sets these (navigation_graph_safe.py:340-345); make_world starts them at 0
+        self.multiple_engagement_rew_scaled = 0
+        self.conflict_rew_scaled = 0
+        self.diff_from_filtered_action_rew_scaled = 0
+        self.conflict_value_rew_scaled = 0
         self.di = g("dynamics_type") == "double_integrator"
         self.C = _DI if self.di else _AT
         self.integrator = integrator
@@ -217,7 +240,7 @@ class OracleEnv:
         self.min_speed = 0.0 if self.di else _AT.V_MIN
         # HJ data (HjDataHandle); tables are inputs (float32 arrays + grid meta)
         self.hj = None
-        if self.use_safety_filter:
+        if self.use_hj:
             t = value_table
             self.hj_grid = Grid(t["lo"], t["hi"], t["shape"], t.get("periodic", ()))
             self.values_hj = np.array(t["values_hj"], dtype=F32, copy=True)
@@ -303,12 +326,19 @@ class OracleEnv:
         self.ghe = self.ghe_init * (1.0 - sl) + self.ghe_target * sl
         self.gse = self.gse_init * (1.0 - st) + self.gse_target * st
         self.min_dist_thresh = self.min_dist_thresh_init * (1.0 - st) + self.min_dist_thresh_target * st
+        # RewardWeightConfig (config.py:64-73) x the stair ratio; a Python int when st is one
+        self.multiple_engagement_rew_scaled = RW_POTENTIAL_CONFLICT * st
+        self.conflict_rew_scaled = RW_SAFETY_VIOLATION * st
+        self.diff_from_filtered_action_rew_scaled = RW_DIFF_FROM_FILTERED_ACTION * st
+        self.conflict_value_rew_scaled = RW_HJ_VALUE * st
         phase = self.stair(start=0.2, end=0.75, num_steps=4) * 0.5 * np.pi
         rsd = 1 - np.cos(phase)
         if self.use_safety_filter:   # INITIAL_PHASE_USE_SAFETY_FILTER is False
             self.world_filter_on = bool(sl > 0)
         self.separation_distance = self.sep_init * (1.0 - rsd) + self.sep_target * rsd
-        if self.use_safety_filter:
+        # world.update_safety_filter_separation_distance shifts the handle whenever one exists
+        # (core.py:483-486), i.e. also with the filter off when HJ_VALUE built it
+        if self.use_hj:
             shift = self.separation_distance - self.hj_sep
             self.values_hj -= shift
             self.hj_sep = self.separation_distance
@@ -668,8 +698,64 @@ class OracleEnv:
             else:
                 self._realistic_update(i)
 
+    # ---- optional reward terms (navigation_graph_safe.py:793-837) -----------------------------
+    # Sequential per agent like the reference: agents a < i already had their goal / done update
+    # in this step (self.done[a] is the updated flag), agents a > i not yet.
+    def _reward_safety_violation(self, i):
+        rew = 0
+        for a in range(self.N):
+            if a != i and np.linalg.norm(self.pos(a) - self.pos(i)) < self.separation_distance and not self.done[a]:
+                rew += self.conflict_rew_scaled
+        return rew
+
+    def _reward_multiple_engagement(self, i):
+        engagement_count = 0
+        engagement_penalty = 0
+        for a in range(self.N):
+            if a != i and np.linalg.norm(self.pos(a) - self.pos(i)) < self.engagement_distance and not self.done[a]:
+                rdv = self.pos(a) - self.pos(i)
+                rd = np.linalg.norm(rdv)
+                close = 1 - np.clip((rd - self.separation_distance) /
+                                    (self.engagement_distance - self.separation_distance), 0, 1)
+                ang = np.arctan2(rdv[1], rdv[0])
+                direction = np.array([np.cos(ang), np.sin(ang)])
+                rel_vel = self.vel(a) - self.vel(i)
+                change = np.inner(direction, rel_vel)
+                change = np.abs(min(0, change))
+                engagement_penalty += change * close
+                engagement_count += 1
+        if engagement_count > 1:
+            return self.multiple_engagement_rew_scaled * engagement_penalty
+        return 0
+
+    def _reward_diff_from_filtered_action(self, i):
+        if not self.done[i]:
+            return self.diff_from_filtered_action_rew_scaled * self.action_diff[i]
+        return 0
+
+    def _reward_hj_value(self, i, eps_hj=0.4):
+        """World.get_hj_value_between_two_agents (core.py:459-468): the handle's interpolated value
+        at get_relative_state(agent, a), +inf when NaN / out of the grid."""
+        rew = 0
+        for a in range(self.N):
+            if a != i and not self.done[a]:
+                v = self.hj_grid.interpolate(self.values_hj, self._rel_state(self.s[i], self.s[a]))
+                if np.isnan(v):
+                    v = np.inf
+                pen = np.abs(min(v - eps_hj, 0))
+                rew += self.conflict_value_rew_scaled * pen
+        return rew
+
     def reward(self, i):
         rew = self.reward_reach_goal(i)
+        if self.rw_safety_violation:
+            rew += self._reward_safety_violation(i)
+        if self.rw_potential_conflict:
+            rew += self._reward_multiple_engagement(i)
+        if self.rw_diff_from_filtered_action and self.use_safety_filter:
+            rew += self._reward_diff_from_filtered_action(i)
+        if self.rw_hj_value:
+            rew += self._reward_hj_value(i)
         if self.realistic:
             self._realistic_update(i)
             return np.clip(rew, MIN_REWARD, MAX_REWARD)
@@ -954,6 +1040,9 @@ class OracleEnv:
             info = {'individual_reward': r}
             info.update(self.info(i))
             infos.append(info)
+        if self.collaborative:   # shared_reward: every agent gets [sum] (environment.py:1031-1037)
+            total = np.sum(rew)
+            rew = [[total]] * self.N
         return obs, aid, node, adj, rew, dones, infos
 
 

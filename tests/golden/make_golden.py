@@ -64,9 +64,31 @@ def _dep_rows(world):
                       float(getattr(a.state, "init_theta", 0.0) or 0.0)] for a in world.agents])
 
 
-def run_case(name, args, seed, ep, steps, value_stored=None, ttr_stored=None, inject=None,
-             action_seed=0, runner_episodes=False, sep_curriculum=False, eval_type=None, image_size=None,
-             dummy=False, full_every=50):
+REWARD_FLAGS = {"safety_violation": "SAFETY_VIOLATION", "potential_conflict": "POTENTIAL_CONFLICT",
+                "diff_from_filtered_action": "DIFF_FROM_FILTERED_ACTION", "hj_value": "HJ_VALUE"}
+
+
+def run_case(name, args, seed, ep, steps, reward_terms=(), **kw):
+    """run_case_ with RewardBinaryConfig's optional reward terms (multiagent/config.py:78-83) switched
+    on for the whole run: make_world reads HJ_VALUE (use_hj_handle, navigation_graph_safe.py:195),
+    every reward call reads all four (:843-850)."""
+    if not reward_terms:
+        return run_case_(name, args, seed, ep, steps, **kw)
+    ref_harness._install_paths()
+    from multiagent.config import RewardBinaryConfig
+    old = {k: getattr(RewardBinaryConfig, v) for k, v in REWARD_FLAGS.items()}
+    for k in reward_terms:
+        setattr(RewardBinaryConfig, REWARD_FLAGS[k], True)
+    try:
+        return run_case_(name, args, seed, ep, steps, reward_terms=tuple(reward_terms), **kw)
+    finally:
+        for k, v in old.items():
+            setattr(RewardBinaryConfig, REWARD_FLAGS[k], v)
+
+
+def run_case_(name, args, seed, ep, steps, value_stored=None, ttr_stored=None, inject=None,
+              action_seed=0, runner_episodes=False, sep_curriculum=False, eval_type=None, image_size=None,
+              dummy=False, full_every=50, reward_terms=()):
     """runner_episodes: step t passes the runner's episode counter ep + t // episode_length, as
     GMPERunner.run does (graph_mpe_runner.py:72-103), so the worker's auto-resets
     (env_wrappers.py:866-871) move through the curriculum. sep_curriculum: the reference's
@@ -188,6 +210,8 @@ def run_case(name, args, seed, ep, steps, value_stored=None, ttr_stored=None, in
     if image_size is not None:
         meta["bayarea_image_size"] = tuple(image_size)
     meta["dummy"] = bool(dummy)
+    if reward_terms:
+        meta["reward_terms"] = tuple(reward_terms)
     out["meta"] = np.array(repr(meta))
     path = os.path.join(HERE, name + ".npz")
     np.savez_compressed(path, **out)
@@ -385,6 +409,38 @@ def main(only=None):
     if only == "collision":
         record_collision_forces()
         return
+    # RewardBinaryConfig's optional reward terms (navigation_graph_safe.py:793-850) and the shared
+    # reward of --collaborative (environment.py:79-80,1031-1037). di_n8_rw_all walks the curriculum
+    # (the runner's episode counter, 8 episodes): the stair ratio is the Python int 0, then float64
+    # 0.25 .. 0.75 ... then the int 1, which decides float32 vs float64 sums of the HJ-value term.
+    every = ("safety_violation", "potential_conflict", "diff_from_filtered_action", "hj_value")
+    rewards = [
+        lambda: run_case("di_n8_rw_all", A(num_agents=8, num_env_steps=30 * 8, episode_length=30,
+                                           use_safety_filter=True),
+                         seed=51, ep=0, steps=240, value_stored=di_small, action_seed=21, runner_episodes=True,
+                         reward_terms=every),
+        lambda: run_case("di_n4_rw_hj_off", A(num_agents=4, num_env_steps=60 * 4, episode_length=60),
+                         seed=52, ep=4, steps=130, value_stored=di_small, action_seed=22,
+                         reward_terms=("safety_violation", "potential_conflict", "hj_value")),
+        lambda: run_case("at_n4_rw_all", A(num_agents=4, num_env_steps=80 * 4, dynamics_type="airtaxi", world_size=6,
+                                           episode_length=80, use_safety_filter=True),
+                         seed=53, ep=4, steps=170, value_stored=at_small, ttr_stored=ttr_small, action_seed=23,
+                         reward_terms=every),
+        lambda: run_case("di_n4_collab", A(num_agents=4, num_env_steps=60 * 4, episode_length=60,
+                                           use_safety_filter=True, collaborative=True),
+                         seed=54, ep=2, steps=130, value_stored=di_small, action_seed=24,
+                         reward_terms=("safety_violation",)),
+        lambda: run_case("di_n8_collab", A(num_agents=8, num_env_steps=40 * 4, episode_length=40,
+                                           collaborative=True), seed=55, ep=1, steps=90, action_seed=25),
+        lambda: run_case("at_n3_collab", A(num_agents=3, num_env_steps=60 * 4, dynamics_type="airtaxi", world_size=6,
+                                           episode_length=60, collaborative=True),
+                         seed=56, ep=4, steps=130, ttr_stored=ttr_small, action_seed=26,
+                         reward_terms=("potential_conflict", "safety_violation")),
+    ]
+    if only == "rewards":
+        for f in rewards:
+            f()
+        return
     if only == "sepcur":
         for f in sepcur:
             f()
@@ -409,6 +465,8 @@ def main(only=None):
     run_case("at_n3_off_ep1", A(num_agents=3, num_env_steps=350 * 4, dynamics_type="airtaxi",
                                 world_size=6, episode_length=350), seed=2, ep=1, steps=120,
              ttr_stored=ttr_small, action_seed=7)
+    for f in rewards:
+        f()
 
 
 if __name__ == "__main__":

@@ -81,7 +81,8 @@ def tables_for(meta):
     from lsm import hj_tables
     di = meta["dynamics_type"] == "double_integrator"
     vt = tt = None
-    if meta["use_safety_filter"]:
+    # HjDataHandle exists with the filter on or RewardBinaryConfig.HJ_VALUE (navigation_graph_safe.py:195)
+    if meta["use_safety_filter"] or "hj_value" in (meta.get("reward_terms") or ()):
         st = hj_tables.synthetic_di_stored((31, 31, 21, 21)) if di else \
             hj_tables.synthetic_airtaxi_stored((25, 25, 24, 7, 7))
         # HjDataHandle is built at the scenario's initial separation: 0 with the separation

@@ -96,3 +96,48 @@ def test_sharded_oracle_envs_equal_global_envs():
         r1 = parts[1].step(a[2:], 2)
         np.testing.assert_array_equal(g[0], np.concatenate([r0[0], r1[0]]))
         np.testing.assert_array_equal(g[4], np.concatenate([r0[4], r1[4]]))
+
+
+def test_init_rank_binds_the_device_before_the_process_group(monkeypatch):
+    """RCCL rank setup (bench.py, INTEGRATION.md factory): torch.cuda.set_device(local_rank) comes
+    BEFORE init_process_group, which gets the same device as device_id, and barriers name it; a
+    communicator created first would bind every rank to GPU 0."""
+    import torch.distributed as dist
+    calls = []
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    monkeypatch.setenv("RANK", "1")
+    monkeypatch.setenv("LOCAL_RANK", "1")
+    monkeypatch.setattr(torch.cuda, "is_available", lambda: True)
+    monkeypatch.setattr(torch.cuda, "set_device", lambda d: calls.append(("set_device", str(d))))
+    monkeypatch.setattr(torch.cuda, "current_device", lambda: 1)
+    state = {"init": False}
+    monkeypatch.setattr(dist, "is_initialized", lambda: state["init"])
+    monkeypatch.setattr(dist, "is_available", lambda: True)
+
+    def fake_init(backend, **kw):
+        calls.append(("init_process_group", backend, str(kw.get("device_id"))))
+        state["init"] = True
+    monkeypatch.setattr(dist, "init_process_group", fake_init)
+    monkeypatch.setattr(dist, "barrier", lambda **kw: calls.append(("barrier", kw.get("device_ids"))))
+    dev = ldist.init_rank("nccl")
+    ldist.barrier("nccl")
+    assert str(dev) == "cuda:1"
+    assert calls == [("set_device", "cuda:1"), ("init_process_group", "nccl", "cuda:1"), ("barrier", [1])]
+
+
+def test_bench_uses_init_rank_and_per_rank_actions():
+    """bench.py joins the process group only through lsm.dist.init_rank (device first), and each
+    rank's synthetic actions are exactly its rows of the single-process draw."""
+    import inspect
+    sys.path.insert(0, os.path.dirname(HERE))
+    import bench
+    src = inspect.getsource(bench.main)
+    assert "init_process_group" not in src and "init_rank(" in src
+    assert src.index("init_rank(") < src.index("GpuGraphVecEnv(")
+    full = bench.synthetic_actions(7, 0, 64, 8, "cpu")
+    assert full.dtype == torch.int32 and int(full.min()) >= 0 and int(full.max()) < 25
+    assert len(torch.unique(full)) == 25
+    for r in range(4):
+        np.testing.assert_array_equal(bench.synthetic_actions(7, 16 * r, 16, 8, "cpu").numpy(),
+                                      full[16 * r:16 * (r + 1)].numpy())
+    assert not torch.equal(bench.synthetic_actions(8, 0, 64, 8, "cpu"), full)

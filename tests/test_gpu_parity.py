@@ -93,6 +93,9 @@ def test_gpu_matches_reference_golden(name, kernel, monkeypatch):
     env.close()
 
 
+ALL_TERMS = ("safety_violation", "potential_conflict", "diff_from_filtered_action", "hj_value")
+
+
 def _oracle_for(meta, seed, n_envs, env_offset=0):
     from oracle.lsm_oracle import OracleVecEnv
     vt, tt = tables_for(meta)
@@ -117,6 +120,18 @@ CASES = [
     # compile-time N = 8 / N = 3 double integrator (rollout_kernel<0, 64, 8> / <0, 64, 3>)
     dict(dynamics_type="double_integrator", num_agents=3, world_size=4, episode_length=60,
          num_env_steps=60 * 4, use_safety_filter=True, ep=4),
+    # RewardBinaryConfig's four optional terms and the shared reward of --collaborative
+    # (navigation_graph_safe.py:793-850, environment.py:1031-1037) through every kernel variant: the
+    # team kernel's agent wave at N = 8 (stair ratio the int 1: float32 HJ-value products) ...
+    dict(dynamics_type="double_integrator", num_agents=8, world_size=4, episode_length=60,
+         num_env_steps=60 * 4, use_safety_filter=True, ep=4, collaborative=True, reward_terms=ALL_TERMS),
+    # ... airtaxi N = 16 mid-curriculum (float64 weights) ...
+    dict(dynamics_type="airtaxi", num_agents=16, world_size=6, episode_length=20,
+         num_env_steps=20 * 4, use_safety_filter=True, ep=2, n_envs=8, collaborative=True,
+         reward_terms=ALL_TERMS),
+    # ... and the HJ-value term with the filter off (the handle exists only for the reward)
+    dict(dynamics_type="double_integrator", num_agents=5, world_size=4, episode_length=60,
+         num_env_steps=60 * 4, use_safety_filter=False, ep=1, reward_terms=("hj_value", "safety_violation")),
 ]
 
 
@@ -151,7 +166,9 @@ def _oracle_run(case):
         a = rng.integers(0, 25, (nb, meta["num_agents"]))
         o = ora.step(a, ep)
         run["steps"].append(dict(a=a, obs=f32(o[0]), node=f32(o[2]), adj=f32(o[3]), rew=np.asarray(o[4]),
-                                 dones=np.asarray(o[5]), state=np.stack([e.s.copy() for e in ora.envs])))
+                                 dones=np.asarray(o[5]), state=np.stack([e.s.copy() for e in ora.envs]),
+                                 ind_rew=np.array([[d["individual_reward"] for d in inf[:meta["num_agents"]]]
+                                                   for inf in o[6]], dtype=np.float64)))
     _ORACLE_RUNS[case] = run
     return run
 
@@ -209,6 +226,8 @@ def test_gpu_matches_oracle_multi_env(case, lpe, monkeypatch):
         np.testing.assert_allclose(g[2], r["node"][:n], rtol=0, atol=F32_ATOL, err_msg=ctx)
         np.testing.assert_allclose(g[3], r["adj"][:n], rtol=0, atol=F32_ATOL, err_msg=ctx)
         np.testing.assert_allclose(g[4], r["rew"][:n], rtol=1e-6, atol=1e-5, err_msg=ctx)
+        np.testing.assert_allclose(env.t_info.cpu().numpy()[:, :, _info_col("individual_reward")],
+                                   r["ind_rew"][:n], rtol=1e-9, atol=1e-9, err_msg=ctx + " individual_reward")
         st = env.state().cpu().numpy()
         np.testing.assert_allclose(st, r["state"][:n], rtol=0, atol=STATE_ATOL, err_msg=ctx)
         mism += int(np.any(st != r["state"][:n], axis=(1, 2)).sum())
@@ -506,23 +525,41 @@ def test_gpu_runner_call_pattern_separation_curriculum(kernel, monkeypatch):
 
 
 @pytest.mark.gpu
-def test_gpu_separation_chain_bound():
-    """The per-env shift chain holds at most 8 separation changes per table upload: a 9th change of
-    the separation across calls is refused with an error (nothing launched), and re-uploading the
-    table starts afresh."""
-    from lsm import capi
-    meta = dict(dynamics_type="double_integrator", num_agents=3, num_landmarks=2, world_size=4,
+@pytest.mark.parametrize("kernel", ["wave", "block"])
+def test_gpu_separation_chain_unbounded(kernel, monkeypatch):
+    """HjDataHandle.update_separation_distance (safety_filter.py:170-174) has no limit: 24 separation
+    changes (alternating stair levels, well past the record's 8 slots: the chain continues in the
+    per-env HBM overflow, grown twice) and the filter after each still matches the oracle, whose
+    table is shifted in place as the reference's is; a re-upload then starts every chain afresh."""
+    if kernel == "block":
+        monkeypatch.setenv("LSM_KERNEL", "block")
+    meta = dict(dynamics_type="double_integrator", num_agents=4, num_landmarks=2, world_size=4,
                 episode_length=5, num_env_steps=5 * 20, n_rollout_threads=1, use_safety_filter=True,
                 use_masking=True, num_internal_step=1, seed=1, env_seed=1, separation_distance_curriculum=True)
-    env = _gpu_env(meta, n_envs=2, seed=1)
-    # stair levels of ep = 0, 4, 8, 12, 16 (0, .25, .5, .75, 1); alternate up and down
-    seq = [4, 8, 12, 16, 12, 8, 4, 8]
-    env.reset(0)
-    for ep in seq:
-        env.reset(ep)
-    with pytest.raises(capi.LsmError, match="separation-distance changes"):
-        env.reset(12)
-    env._upload_value_table()
+    n = 3
+    env = _gpu_env(meta, n_envs=n, seed=1)
+    ora = _oracle_for(meta, 1, n)
+    # stair levels of ep = 0, 4, 8, 12, 16 (0, .25, .5, .75, 1); up and down, 24 changes
+    seq = [0] + [4, 8, 12, 16, 12, 8, 4, 8] * 3
+    rng = np.random.default_rng(3)
+    for k, ep in enumerate(seq):
+        g, o = env.reset(ep), ora.reset(ep)
+        np.testing.assert_allclose(g[0], o[0], rtol=0, atol=F32_ATOL)
+        for t in range(3):
+            a = rng.integers(0, 25, (n, meta["num_agents"]))
+            g, o = env.step(a, ep), ora.step(a, ep)
+            ctx = "reset %d (ep %d) step %d" % (k, ep, t)
+            np.testing.assert_array_equal(g[5], o[5], err_msg=ctx)
+            np.testing.assert_allclose(g[0], o[0], rtol=0, atol=F32_ATOL, err_msg=ctx)
+            np.testing.assert_allclose(env.state().cpu().numpy(), np.stack([e.s for e in ora.envs]), rtol=0,
+                                       atol=STATE_ATOL, err_msg=ctx)
+            info = env.t_info.cpu().numpy()
+            np.testing.assert_array_equal(info[:, :, _info_col("deconflicting_agent_index")].astype(int),
+                                          np.stack([e.deconflicting for e in ora.envs]), err_msg=ctx)
+            np.testing.assert_array_equal(info[:, :, _info_col("Safety filtered")].astype(bool),
+                                          np.stack([e.safety_filtered for e in ora.envs]), err_msg=ctx)
+    assert env.lib.lsm_kernel_name(env.h)
+    env._upload_value_table()   # a new HjDataHandle: chains start empty, nothing refused
     env.reset(12)
     env.close()
 
@@ -645,16 +682,21 @@ def test_gpu_collision_forces_reported_never_applied(kernel, monkeypatch):
     off.close()
 
 
-@pytest.mark.parametrize("team", ["4", "2", "8"])
+@pytest.mark.parametrize("team", ["4", "2", "8", "4s"])
 @pytest.mark.parametrize("dyn,N", [("double_integrator", 8), ("airtaxi", 16)])
 def test_gpu_team_kernel_resets_match_oracle(dyn, N, team, monkeypatch):
     """The team kernel's auto-resets (all of a workgroup's envs, or some, reset in one launch; the
     scenario draws run one lane per env from the staged MT19937 stream, crossing block boundaries
     over successive resets) against the oracle: 10-step episodes, 75 steps (7 resets per env),
-    envs driven all-done early at different steps so resets do not line up, every output."""
+    envs driven all-done early at different steps so resets do not line up, every output. "4s":
+    the lane streams hold only 40 words (LSM_MT_STAGE), so every draw runs out and takes the
+    cooperative redraw, whose stream state goes back to HBM."""
     import torch
     if dyn == "airtaxi" and team == "8":
         pytest.skip("8 airtaxi envs of 16 agents do not fit one 64-lane agent wave")
+    if team == "4s":
+        monkeypatch.setenv("LSM_MT_STAGE", "40")
+        team = "4"
     monkeypatch.setenv("LSM_TEAM", team)
     ws = 4 if dyn == "double_integrator" else 6
     meta = dict(dynamics_type=dyn, num_agents=N, num_landmarks=2, world_size=ws, episode_length=10,
