@@ -209,7 +209,7 @@ void rollout_block_kernel(const KParams* __restrict__ Pp, const KStep K) {
   RTSTAMP(13);
 #ifdef LSM_STAMPS
   if (tid == 0 && gptr(P.stamps))
-    gptr(P.stamps)[(size_t)env * 16 + 15] = (unsigned long long)__builtin_amdgcn_s_getreg(63492) |
+    gptr(P.stamps)[(size_t)env * LSM_NSTAMP + 15] = (unsigned long long)__builtin_amdgcn_s_getreg(63492) |
                                       ((unsigned long long)__builtin_amdgcn_s_getreg(6164) << 32);
 #endif
   STAMP(0);

@@ -53,19 +53,25 @@
 #define LSM_HOST_PART 1
 #endif
 
+// stamps per env in LSM_OUT_DEBUG_STAMPS: 16 in the ABI; diagnostic builds stamp 32
+#ifdef LSM_STAMPS
+#define LSM_NSTAMP 32
+#else
+#define LSM_NSTAMP 16
+#endif
 #ifdef LSM_STAMPS
 // diagnostic build only: per-phase s_memtime stamps of each env's wave (never in the product .so)
 #define STAMP(k)                                                                             \
   do {                                                                                       \
     __syncthreads();                                                                         \
-    if (lane == 0 && gptr(P.stamps)) gptr(P.stamps)[(size_t)env * 16 + (k)] = __builtin_amdgcn_s_memtime(); \
+    if (lane == 0 && gptr(P.stamps)) gptr(P.stamps)[(size_t)env * LSM_NSTAMP + (k)] = __builtin_amdgcn_s_memtime(); \
     if (K.stop_after == (k)) return;  /* per-phase instruction counting (lsm.diag_stamps) */ \
   } while (0)
 // slots 13/14: 100 MHz chip-wide clock at wave start / end (dispatch ramp and tail);
 // slot 15: HW_ID (wave, simd, cu, se) | XCC_ID << 32
 #define RTSTAMP(k)                                                                           \
   do {                                                                                       \
-    if (lane == 0 && gptr(P.stamps)) gptr(P.stamps)[(size_t)env * 16 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+    if (lane == 0 && gptr(P.stamps)) gptr(P.stamps)[(size_t)env * LSM_NSTAMP + (k)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
 #else
 #define RTSTAMP(k) \
@@ -2913,7 +2919,7 @@ __global__ __launch_bounds__(64, DYN == 0 ? (LPE == 64 ? 4 : 2) : LSM_WAVES_PER_
   RTSTAMP(13);
 #ifdef LSM_STAMPS
   if (lane == 0 && gptr(P.stamps))
-    gptr(P.stamps)[(size_t)env * 16 + 15] = (unsigned long long)__builtin_amdgcn_s_getreg(63492) |
+    gptr(P.stamps)[(size_t)env * LSM_NSTAMP + 15] = (unsigned long long)__builtin_amdgcn_s_getreg(63492) |
                                       ((unsigned long long)__builtin_amdgcn_s_getreg(6164) << 32);
 #endif
   STAMP(0);
@@ -3049,7 +3055,8 @@ __global__ __launch_bounds__(64, DYN == 0 ? (LPE == 64 ? 4 : 2) : LSM_WAVES_PER_
   // ego's mask is the pre-update mask, so the adjacency can be stored now, in four chunks of
   // egos placed between the remaining phases: the stores drain while the wave computes
   // instead of queueing behind each other at the end. A status change rewrites it at the end.
-  const bool chunked = (E & 3) == 0 && !P.adj_compact && !S.dep0;
+  // (not for an env that auto-resets at the episode-length boundary: the reset emits its outputs)
+  const bool chunked = (E & 3) == 0 && !P.adj_compact && !S.dep0 && !(P.auto_reset && cstep >= P.episode_length);
   const uint64_t m_pre = chunked ? ego_mask(S, N, L, -1) : 0;
   if (chunked) emit_adj_uniform<LPE, NT>(P, S, env, m_pre, 0, N / 4);
   STAMP(6);
@@ -3413,7 +3420,7 @@ size_t lsm_output_bytes(const lsm_env* e, int32_t slot) {
     case LSM_OUT_INFO: return n * N * LSM_INFO_FIELDS * 8;
     case LSM_OUT_EDGES: return n * E * E;
     case LSM_OUT_STATE: return n * N * 4 * 8;
-    case LSM_OUT_DEBUG_STAMPS: return n * 16 * 8;
+    case LSM_OUT_DEBUG_STAMPS: return n * LSM_NSTAMP * 8;
     case LSM_OUT_SHARE_OBS: return n * N * N * e->OBS * 4;
     case LSM_OUT_MASKS: return n * N * 4;
     case LSM_OUT_ACTIVE_MASKS: return n * N * 4;

@@ -43,11 +43,11 @@ __host__ __device__ inline size_t team_env_bytes(size_t bytes, int N) {
 #ifdef LSM_STAMPS
 #define TSTAMP(k)                                                                                  \
   do {                                                                                             \
-    if (lane == 0 && live && gptr(P.stamps)) gptr(P.stamps)[(size_t)env * 16 + (k)] = __builtin_amdgcn_s_memtime(); \
+    if (lane == 0 && live && gptr(P.stamps)) gptr(P.stamps)[(size_t)env * LSM_NSTAMP + (k)] = __builtin_amdgcn_s_memtime(); \
   } while (0)
 #define TRTSTAMP(k)                                                                                \
   do {                                                                                             \
-    if (lane == 0 && live && gptr(P.stamps)) gptr(P.stamps)[(size_t)env * 16 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+    if (lane == 0 && live && gptr(P.stamps)) gptr(P.stamps)[(size_t)env * LSM_NSTAMP + (k)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
 #else
 #define TSTAMP(k) do { } while (0)
@@ -204,7 +204,7 @@ void rollout_team_kernel(const KParams* __restrict__ Pp, const KStep K) {
   TSTAMP(0);
 #ifdef LSM_STAMPS
   if (lane == 0 && live && gptr(P.stamps))
-    gptr(P.stamps)[(size_t)env * 16 + 15] = (unsigned long long)__builtin_amdgcn_s_getreg(63492) |
+    gptr(P.stamps)[(size_t)env * LSM_NSTAMP + 15] = (unsigned long long)__builtin_amdgcn_s_getreg(63492) |
                                           ((unsigned long long)__builtin_amdgcn_s_getreg(6164) << 32);
 #endif
 
@@ -287,10 +287,12 @@ void rollout_team_kernel(const KParams* __restrict__ Pp, const KStep K) {
         S.vpair[p] = ok ? v : INFINITY;
         S.inr[p] = ok ? 1 : 0;
       }
+      TSTAMP(16);
       // the deconflicting choice and the HJ gradient lookup of every ego, here where the other
       // waves of the SIMD hide the gather; the agent wave does the QP in B (filter_agent_slot)
       esync<LPE>();
       if (lane < N) filter_prep<DYN, NT>(P, S, lane);
+      TSTAMP(17);
     }
   }
   TSTAMP(6);
@@ -331,7 +333,9 @@ void rollout_team_kernel(const KParams* __restrict__ Pp, const KStep K) {
   TSTAMP(2);
 
   // ---- C. distances; contact forces and magnetic-field sums when asked ------------------------
-  const bool chunked = (E & 3) == 0 && !P.adj_compact;
+  // the speculative adjacency stores of phase D are skipped for an env that auto-resets at the
+  // episode-length boundary (known from the step count): the reset emits its outputs instead
+  const bool chunked = (E & 3) == 0 && !P.adj_compact && !(P.auto_reset && cstep >= P.episode_length);
   uint64_t m_pre = 0;
   if (live) {
     compute_dist<LPE, NT>(P, S, PRE ? prw : nullptr);
@@ -404,6 +408,7 @@ void rollout_team_kernel(const KParams* __restrict__ Pp, const KStep K) {
     const bool all_done = __all(my_done);
     write_masks(P, env, N, lane, my_done, all_done);
     esync<LPE>();   // info rows read out of U2 before the node rows / a reset overwrite it
+    TSTAMP(18);
     if (lane == 0) { S.step[0] = cstep; S.step[1] = 0; }
     rs = P.auto_reset && all_done;
     if (lane == 0) gptr(P.o.reset_flag)[env] = rs ? 1 : 0;
@@ -424,16 +429,20 @@ void rollout_team_kernel(const KParams* __restrict__ Pp, const KStep K) {
   if (nrs != 0) {   // workgroup-uniform
     int p0 = 0;
     if (rs) p0 = team_reset_prep<DYN, NT>(P, S, env, K.cur_new);
+    TSTAMP(19);
     __syncthreads();
     // (each env's wave drawing its own env on one lane measured slower: reset steps 85.7-89.1 vs
     // 79.8-85.9 us, profiles/r03_v19_reset_*.json)
     if (w == 0 && lane < G && team_rs[lane]) team_scenario<DYN, NT>(P, smem, B, lane, env0 + lane);
     __syncthreads();
+    TSTAMP(20);
     if (rs) {
       team_reset_finish<DYN, NT>(P, S, env, p0);
       compute_dist<LPE, NT>(P, S, nullptr, true);
+      TSTAMP(21);
       if (lane < N) write_obs<DYN, NT>(P, S, env, lane);
       emit_graph<DYN, LPE, NT>(P, S, env);
+      TSTAMP(22);
       esync<LPE>();
       store_state<DYN, LPE, NT>(P, S, lbase, env, true);
     }

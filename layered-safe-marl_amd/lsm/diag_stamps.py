@@ -52,7 +52,7 @@ def main():
     n_envs = a.envs or c["envs"]
     env = GpuGraphVecEnv(args, num_envs=n_envs, device="cuda:0", value_table=vt, ttr_table=tt,
                          return_numpy=False, build_infos=False, adj_layout=c.get("adj_layout", "reference"))
-    stamps = torch.zeros((n_envs, 16), dtype=torch.int64, device="cuda:0")
+    stamps = torch.zeros((n_envs, 32), dtype=torch.int64, device="cuda:0")   # LSM_NSTAMP
     capi.check(env.lib.lsm_bind_output(env.h, capi.OUT_DEBUG_STAMPS, C.c_void_p(stamps.data_ptr()),
                                        stamps.numel() * 8), env.h)
     env.reset(4)
@@ -67,7 +67,7 @@ def main():
             hw = raw[:, 15].astype(np.uint64)   # HW_ID | XCC_ID << 32 of this step's waves
             s = raw.astype(np.float64)
             tstamps.append(s[:, :9].copy())
-            tstamps12.append(s[:, :13].copy())
+            tstamps12.append(s[:, :32].copy())
             stamps.zero_()
             acc.append(np.diff(s[:, [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10]], axis=1))
             t0 = s[:, 13].min()
@@ -97,9 +97,12 @@ def main():
         print("late2% " + " ".join("%10.0f" % np.median(allst[late, j] - allst[late, i]) for _, i, j in segs) +
               "  %10.2f  slots %s" % (np.median(rts[late]) / 1e3, np.bincount(slots[late], minlength=G).tolist()))
         ag = np.concatenate(tstamps12, axis=0)
-        for name, i, j in [("A record", 0, 12), ("A decode+pairs", 12, 6), ("B filter", 1, 9),
+        for name, i, j in [("A record", 0, 12), ("A decode+pairs", 12, 16), ("A argmin+grad", 16, 17),
+                           ("A decode..prep", 12, 6), ("B filter", 1, 9),
                            ("B integrate", 9, 2), ("D reward", 3, 10),
-                           ("D info", 10, 11), ("D rows+stats", 11, 8)]:
+                           ("D info", 10, 11), ("D rows+stats", 11, 8), ("E info/dones", 4, 18),
+                           ("E graph+record", 18, 5), ("R prep", 18, 19), ("R prep->draws", 19, 20),
+                           ("R finish+dist", 20, 21), ("R emit", 21, 22), ("R store", 22, 5)]:
             v = ag[:, j] - ag[:, i]
             v = v[(ag[:, i] != 0) & (ag[:, j] != 0)]
             print("%-18s %12.0f   (agent-wave rows: %d)" % (name, np.median(v), len(v)))
