@@ -208,6 +208,8 @@ struct KParams {
 struct KStep {
   const void* actions;
   const double* layout;   // mode 2: [n][layout doubles] (lsm_reset_layout)
+  const float4* rec;      // StateDev::rec and its strides, in the arguments so the first loads of a
+  uint32_t rec_stride16, rec16, a2_16;   // launch need no dependent load of KParams
   int action_kind, mode, emit_edges, stop_after;   // mode 0 = step, 1 = reset all, 2 = reset from layout
   double cur_new[NCUR];
 };
@@ -1618,19 +1620,21 @@ __device__ __forceinline__ void emit_adj_uniform(const KParams& P, const Lds& S,
 template <int DYN, int LPE, int NT>
 __device__ __forceinline__ void emit_nodes(const KParams& P, Lds& S, int env, bool uni);
 
-// `adj_done`: the uniform adjacency was already stored (speculatively, in chunks during the
-// step); it is rewritten here only if an agent changed status.
+// `adj_done` / `nodes_done`: the uniform adjacency / node_obs were already stored (speculatively,
+// earlier in the step); they are rewritten here only if an agent changed status.
 template <int DYN, int LPE, int NT>
-__device__ __forceinline__ void emit_graph(const KParams& P, Lds& S, int env, bool adj_done = false) {
+__device__ __forceinline__ void emit_graph(const KParams& P, Lds& S, int env, bool adj_done = false,
+                                           bool nodes_done = false) {
   const int lane = threadIdx.x & (LPE - 1);
   LSM_DIMS;
-  if (DYN == 0) build_rows_di<LPE, NT>(P, S); else trig_table_at<LPE, NT>(P, S);
-  esync<LPE>();
   // No agent changed done / reached status this step (the common case): every ego then has
   // the same disconnect mask and the same (pre == post) entity rows, so each lane computes
   // its output words once and stores them for all N egos.
   const bool uni = !S.dep0 &&
                    group_all<LPE>(lane >= N || (S.dpre[lane] == S.dpost[lane] && S.rpre[lane] == S.rpost[lane]));
+  if (uni && adj_done && nodes_done) return;
+  if (DYN == 0) build_rows_di<LPE, NT>(P, S); else trig_table_at<LPE, NT>(P, S);
+  esync<LPE>();
   // ---- adjacency: ego e, row r, col c ------------------------------------------------------
   const int EE = E * E, atot = N * EE;
   GAS float* adj_out = gptr(P.o.adj) + (size_t)env * atot;
@@ -1693,7 +1697,7 @@ __device__ __forceinline__ void emit_graph(const KParams& P, Lds& S, int env, bo
       adj_out[q] = (((m >> r) | (m >> c)) & 1ull) ? 0.0f : fv1(S, N, NL, E, r, c);
     }
   }
-  emit_nodes<DYN, LPE, NT>(P, S, env, uni);
+  if (!(uni && nodes_done)) emit_nodes<DYN, LPE, NT>(P, S, env, uni);
 }
 
 // node_obs [N][E][F] of one env (DI rows / airtaxi trig table already in LDS). `uni`: no
@@ -3866,6 +3870,10 @@ static int launch(lsm_env* e, KStep& L, hipStream_t st) {
     HIPCHK(e, hipStreamSynchronize(st));
     e->params_dirty = false;
   }
+  L.rec = e->s.rec;
+  L.rec_stride16 = e->s.rec_stride16;
+  L.rec16 = e->s.rec16;
+  L.a2_16 = e->s.a2_16;
   L.stop_after = -1;
 #ifdef LSM_STAMPS
   if (const char* v = getenv("LSM_STOP_AFTER")) L.stop_after = atoi(v);

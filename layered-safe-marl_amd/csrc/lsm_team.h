@@ -219,6 +219,19 @@ void rollout_team_kernel(const KParams* __restrict__ Pp, const KStep K) {
   int cstep = 0;
   bool filter_on = false;
   if (live) {
+#ifdef LSM_AB_PRO
+    // the record's loads first, into registers, from the address in the kernel arguments (no
+    // dependent load of the device-resident KParams): the action / pair-word loads issued after
+    // them are younger, so waiting for the record does not wait for them (vmcnt counts in order)
+    const int n16 = split ? (int)K.a2_16 : (int)K.rec16;
+    const GAS f32x4* rsrc = (const GAS f32x4*)K.rec + (size_t)env * K.rec_stride16;
+    f32x4 rr[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int k = lane + q * LPE;
+      if (q * LPE < n16) rr[q] = rsrc[k < n16 ? k : n16 - 1];
+    }
+#endif
     if (K.mode == 0 && lane < N) act = read_action(K, env, N, lane);
     if (PRE) {
 #pragma unroll
@@ -229,8 +242,16 @@ void rollout_team_kernel(const KParams* __restrict__ Pp, const KStep K) {
     }
     // a plain step needs [0, a2) of the record before its distances; the rest (statistics,
     // landmarks) comes in phase B (cold_loads). Resets and the edge output read it all here.
+#ifdef LSM_AB_PRO
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int k = lane + q * LPE;
+      if (q * LPE < n16 && k < n16) ((f32x4*)lbase)[k] = rr[q];
+    }
+#else
     rec_copy<LPE>((const GAS f32x4*)gptr(P.s.rec) + (size_t)env * P.s.rec_stride16, (f32x4*)lbase,
                   split ? P.s.a2_16 : P.s.rec16);
+#endif
     esync<LPE>();
     TSTAMP(12);
     if (lane < N) {
@@ -336,8 +357,23 @@ void rollout_team_kernel(const KParams* __restrict__ Pp, const KStep K) {
   // the speculative adjacency stores of phase D are skipped for an env that auto-resets at the
   // episode-length boundary (known from the step count): the reset emits its outputs instead
   const bool chunked = (E & 3) == 0 && !P.adj_compact && !(P.auto_reset && cstep >= P.episode_length);
+#if defined(LSM_AB_NODEC) || defined(LSM_AB_NODEC0)
+  const bool nodes_c = DYN == 0 && ((E * F) & 3) == 0 && !(P.auto_reset && cstep >= P.episode_length);
+#else
+  constexpr bool nodes_c = false;
+#endif
   uint64_t m_pre = 0;
   if (live) {
+#ifdef LSM_AB_NODEC0
+    // the env's node_obs first thing in C (they need only the integrated positions), speculatively
+    // as below
+    if (nodes_c) {
+      build_rows_di<LPE, NT>(P, S);
+      esync<LPE>();
+      emit_nodes_uniform_di<LPE, NT>(P, S, env, 0, N);
+      esync<LPE>();
+    }
+#endif
     compute_dist<LPE, NT>(P, S, PRE ? prw : nullptr);
     if (P.o.cforce && lane < N) {
       double fx, fy;
@@ -346,6 +382,16 @@ void rollout_team_kernel(const KParams* __restrict__ Pp, const KStep K) {
       cf[0] = fx;
       cf[1] = fy;
     }
+#ifdef LSM_AB_NODEC
+    // the env's node_obs, speculatively: no agent has changed status yet (dpost == dpre here), so
+    // these are the step's rows unless phase D changes one -- phase E then re-emits everything
+    if (nodes_c) {
+      build_rows_di<LPE, NT>(P, S);
+      esync<LPE>();
+      emit_nodes_uniform_di<LPE, NT>(P, S, env, 0, N);
+      esync<LPE>();   // U2 rows read before the magnetic partials overwrite them
+    }
+#endif
     // the magnetic-field segment sums (partials in U2, read by the agent wave in D, before the
     // info rows reuse U2)
     if (DYN == 0 && !P.use_filter_arg) magnetic_partials_wave<LPE, NT>(P, S, S.dpair);
@@ -415,7 +461,7 @@ void rollout_team_kernel(const KParams* __restrict__ Pp, const KStep K) {
     if (!rs) {
       // adjacency already stored in D except WD's (emit_graph rewrites it if a status changed)
 #ifndef LSM_XP_NOOUT
-      emit_graph<DYN, LPE, NT>(P, S, env, chunked && w != WD);
+      emit_graph<DYN, LPE, NT>(P, S, env, chunked && w != WD, nodes_c);
 #endif
       esync<LPE>();
       store_state<DYN, LPE, NT>(P, S, lbase, env, false);

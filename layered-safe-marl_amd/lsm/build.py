@@ -76,9 +76,9 @@ def _run_parallel(jobs, verbose=True):
         raise RuntimeError("compile failed: %s" % ", ".join(os.path.basename(f) for f in failed))
 
 
-def _rollout_jobs(defines=(), tag="", force=True):
+def _rollout_jobs(defines=(), tag="", force=True, parts=None):
     jobs = []
-    for part in range(ROLLOUT_PARTS):
+    for part in (range(ROLLOUT_PARTS) if parts is None else parts):
         o = _part_obj(part, tag)
         if force or _stale(o, _rollout_deps()):
             cmd = [HIPCC] + FLAGS + ["-D%s" % d for d in defines] + ["-DLSM_PART=%d" % part, "-c", "-o", o + ".tmp",
@@ -122,22 +122,25 @@ def variant_path(name: str) -> str:
 def build_variants(specs, verbose: bool = True):
     """A/B experiments and diagnostic builds: the rollout TU rebuilt with extra -D flags and linked
     with the product's other objects into csrc/liblsm_rollout_<name>.so (select it with LSM_LIB=...).
-    Never the product library. specs: ["NAME:D1,D2", ...]; all parts of all variants compile in
-    parallel."""
+    Never the product library. specs: ["NAME:D1,D2", ...], or "NAME:D1,D2@3,4" to recompile only
+    those kernel groups (the others are the product's objects: for defines that only touch those
+    groups' kernels); all recompiled parts of all variants compile in parallel."""
     build(verbose=verbose)
     jobs, variants = [], []
     for spec in specs:
-        name, _, defs = spec.partition(":")
+        name, _, rest = spec.partition(":")
+        defs, _, only = rest.partition("@")
         defines = [d for d in defs.split(",") if d] + [DIAG_DEFINE]
-        jobs += _rollout_jobs(defines, tag="_" + name)
-        variants.append(name)
+        parts = sorted({int(x) for x in only.split(",") if x}) if only else list(range(ROLLOUT_PARTS))
+        jobs += _rollout_jobs(defines, tag="_" + name, parts=parts)
+        variants.append((name, parts))
     _run_parallel(jobs, verbose)
-    for name in variants:
-        parts = [_part_obj(p, "_" + name) for p in range(ROLLOUT_PARTS)]
-        _link(parts + [_obj(u) for u in UNITS], variant_path(name), verbose)
-        for o in parts:
-            os.remove(o)
-    return [variant_path(n) for n in variants]
+    for name, parts in variants:
+        objs = [_part_obj(p, "_" + name) if p in parts else _part_obj(p) for p in range(ROLLOUT_PARTS)]
+        _link(objs + [_obj(u) for u in UNITS], variant_path(name), verbose)
+        for p in parts:
+            os.remove(_part_obj(p, "_" + name))
+    return [variant_path(n) for n, _ in variants]
 
 
 def build_variant(name: str, defines, verbose: bool = True) -> str:
