@@ -108,6 +108,179 @@ struct LaneMT {
   }
 };
 
+// ---- the scenario draw on a whole wave (one env per wave) -----------------------------------
+// random_scenario (lsm_scenario.h) consumes its stream strictly in order, but only its rejection
+// loops (randomly_generate_separated_positions, utils.py:39-68) make the consumption data-dependent,
+// and every draw's words are known once the loops before it are resolved. So the wave computes
+// every fixed-count draw of a stretch on separate lanes, and each rejection loop as 64 tries at once
+// (try j on lane j, words c + 4 j): the first accepted try (a ballot) is the one the sequential
+// loop stops at. Same words, same float64 operations, same values as the one-lane replay.
+//
+// Stream views: word k (k >= 0) of the env's stream from the reset's start position.
+struct MtView {   // the staged MT19937 blocks (team_reset_prep): current from p0, then the next
+  const uint32_t* key;
+  const uint32_t* nxt;
+  int p0, avail;   // words available from p0 (lane draws beyond avail are flagged by the caller)
+  __device__ __forceinline__ uint32_t word(int k) const {
+    const int a = p0 + k;
+    const uint32_t y = a < MT_N ? key[a] : (a < 2 * MT_N ? nxt[a - MT_N] : 0u);
+    return mt_temper(y);
+  }
+};
+struct PhiloxView {   // LSM_RNG_PHILOX: word k = element k % 4 of counter block k / 4
+  uint32_t key, ridx;
+  int avail;
+  __device__ __forceinline__ uint32_t word(int k) const {
+    const uint32_t ctr[4] = {(uint32_t)k >> 2, ridx, 0u, 0u}, kk[2] = {key, 0x4c534d31u};
+    uint32_t o[4];
+    philox4x32_10(ctr, kk, o);
+    const int e = k & 3;
+    return e == 0 ? o[0] : e == 1 ? o[1] : e == 2 ? o[2] : o[3];
+  }
+};
+// RandomState.uniform(lo, hi) from words k, k + 1 (numpy's random_sample)
+template <class V>
+__device__ __forceinline__ double view_uniform(const V& v, int k, double lo, double hi) {
+  const uint32_t a = v.word(k) >> 5, b = v.word(k + 1) >> 6;
+  const double range = hi - lo;
+  return lo + range * ((a * 67108864.0 + b) / 9007199254740992.0);
+}
+
+// random_scenario on the 64 lanes of one wave. Returns the words consumed (> v.avail: the staged
+// stream ran out and the caller redraws sequentially). ws: the scenario workspace (SCEN_WS).
+template <class V>
+__device__ int random_scenario_wave(const V& v, const ScenarioParams& p, double* st, double* lm, double* ws) {
+  const int lane = threadIdx.x & 63;
+  const int N = p.N, L = p.L, NL = N * L;
+  const double wsz = p.world_size, cra = p.ratio_airtaxi, cr = p.ratio_scenario;
+  double* gp = ws;                  // [L][2] (lsm_scenario.h's workspace layout)
+  double* prev = ws + 2 * MAX_L;    // [L][2]
+  double* heads = ws + 4 * MAX_L;   // [L]
+  double* speeds = ws + 5 * MAX_L;  // [L]
+  int c = 0;
+  // agent states: a fixed 4 (DI) / 8 (airtaxi) words per agent, agent i on lane i
+  const int per = p.dyn == 0 ? 4 : 8;
+  for (int i = lane; i < N; i += 64) {
+    const int k = c + per * i;
+    if (p.dyn == 0) {
+      const double x = view_uniform(v, k, -0.8 * wsz, 0.8 * wsz);
+      const double y = view_uniform(v, k + 2, -0.8 * wsz, 0.8 * wsz);
+      st[0 * N + i] = x; st[1 * N + i] = y; st[2 * N + i] = 0.0; st[3 * N + i] = 0.0;
+    } else {
+      const double xmin = -0.5 * wsz;
+      const double xmax = 0.25 * wsz * cra + 0.0 * (1 - cra) * wsz;
+      const double y = view_uniform(v, k, -0.5 * wsz, 0.5 * wsz);
+      const double x = view_uniform(v, k + 2, xmin, xmax);
+      const double spd = view_uniform(v, k + 4, p.goal_speed_min, p.goal_speed_max);
+      const double th = view_uniform(v, k + 6, 0.0, p.two_pi);
+      st[0 * N + i] = x; st[1 * N + i] = y; st[2 * N + i] = th; st[3 * N + i] = spd;
+    }
+  }
+  c += per * N;
+  double x0, x1, y0, y1, dmin, dmax;
+  if (p.dyn == 0) {
+    x0 = -0.5 * wsz; x1 = 0.5 * wsz; y0 = -0.5 * wsz; y1 = 0.5 * wsz;
+    dmin = 0.25 * p.coordination_range; dmax = 0.75 * p.coordination_range;
+  } else {
+    const double yw = 0.1 * (1 - cra) + 0.5 * cra;
+    x0 = 0.0; x1 = 0.75 * wsz; y0 = -yw * wsz; y1 = yw * wsz;
+    dmin = 0.5 * p.coordination_range; dmax = p.coordination_range;
+  }
+  for (int i = 0; i < N; ++i) {
+    // separated_positions: point 0, then one rejection loop per further point
+    if (lane == 0) {
+      gp[0] = view_uniform(v, c, x0, x1);
+      gp[1] = view_uniform(v, c + 2, y0, y1);
+    }
+    c += 4;
+    esync<64>();
+    for (int q = 1; q < L; ++q) {
+      int acc = -1;
+      for (int base = 0; base < 1000 && acc < 0; base += 64) {
+        const int j = base + lane;
+        double x = 0.0, y = 0.0;
+        bool ok = false;
+        if (j < 1000) {
+          x = view_uniform(v, c + 4 * j, x0, x1);
+          y = view_uniform(v, c + 4 * j + 2, y0, y1);
+          double d = 0.0;
+          for (int k = 0; k < q; ++k) {
+            const double dx = gp[2 * k] - x, dy = gp[2 * k + 1] - y;
+            const double dk = sqrt(dx * dx + dy * dy);
+            if (k == 0 || dk < d) d = dk;
+          }
+          ok = (d > dmin && d < dmax) || j == 999;   // the 1000th try is kept whatever it is
+        }
+        const uint64_t m = __ballot(ok);
+        if (m) {
+          const int t = __ffsll((unsigned long long)m) - 1;
+          acc = base + t;
+          const double ax = __shfl(x, t), ay = __shfl(y, t);
+          if (lane == 0) {
+            gp[2 * q] = ax;
+            gp[2 * q + 1] = ay;
+          }
+        }
+      }
+      c += 4 * (acc + 1);
+      esync<64>();
+    }
+    // the previous agent's goals, each kept with probability 1/2 (a draw each)
+    if (i > 0) {
+      if (lane < L && view_uniform(v, c + 2 * lane, 0.0, 1.0) < 0.5) {
+        gp[2 * lane] = prev[2 * lane];
+        gp[2 * lane + 1] = prev[2 * lane + 1];
+      }
+      c += 2 * L;
+      esync<64>();
+    }
+    if (lane == 0) {
+      if (p.dyn != 0 && gp[0] > gp[2]) {
+        const double tx = gp[0], ty = gp[1];
+        gp[0] = gp[2]; gp[1] = gp[3];
+        gp[2] = tx; gp[3] = ty;
+      }
+    }
+    esync<64>();
+    if (lane < L - 1) heads[lane] = atan2(gp[2 * lane + 3] - gp[2 * lane + 1], gp[2 * lane + 2] - gp[2 * lane]);
+    // speeds: the double integrator draws L goal speeds and one switch
+    const int cs = c;
+    if (p.dyn == 0) c += 2 * L + 2;
+    esync<64>();
+    const double last = heads[L - 2];
+    if (p.dyn != 0) {
+      if (lane < L) speeds[lane] = p.goal_speed_max * 1.0;
+    } else {
+      const double var = view_uniform(v, cs + 2 * L, 0.0, 1.0);
+      const bool use_rnd = var < py_min(cr, 1 - 0.2);
+      if (lane < L) {
+        const double r = view_uniform(v, cs + 2 * lane, p.goal_speed_min, p.goal_speed_max);
+        double sp = use_rnd ? r : p.goal_speed_max * 1.0;
+        if (!use_rnd && lane == L - 1) sp = p.goal_speed_min;
+        speeds[lane] = sp;
+      }
+    }
+    // heading noise, one draw per leg
+    const double pr = (p.dyn == 0) ? cr * 0.25 * p.pi : cra * 0.1 * p.pi;
+    if (lane < L - 1) heads[lane] += view_uniform(v, c + 2 * lane, -pr, pr);
+    c += 2 * (L - 1);
+    esync<64>();
+    if (lane == 0) heads[L - 1] = last;
+    esync<64>();
+    if (lane < L) {
+      const int idx = lane * N + i;
+      lm[0 * NL + idx] = gp[2 * lane];
+      lm[1 * NL + idx] = gp[2 * lane + 1];
+      lm[2 * NL + idx] = heads[lane];
+      lm[3 * NL + idx] = speeds[lane];
+      prev[2 * lane] = gp[2 * lane];
+      prev[2 * lane + 1] = gp[2 * lane + 1];
+    }
+    esync<64>();
+  }
+  return c;
+}
+
 // env wave: summary, curriculum, shift; the MT19937 stream staged in LDS (start pos kept)
 template <int DYN, int NT>
 __device__ __forceinline__ int team_reset_prep(const KParams& P, Lds& S, int env, const double* cur_new) {
@@ -145,6 +318,35 @@ __device__ __forceinline__ void team_scenario(const KParams& P, unsigned char* s
   rng.over = false;
   random_scenario(rng, sp, S.ps, S.lm, S.scen);
   S.mt[MT_N] = rng.over ? MT_OVER : (uint32_t)rng.pos;
+}
+
+// env wave: its own env's scenario on the whole wave (random_scenario_wave), from the staged
+// MT19937 blocks (or the Philox stream); S.mt[MT_N] = the new position, MT_OVER if it ran out
+template <int DYN, int NT>
+__device__ __forceinline__ void team_scenario_wave(const KParams& P, Lds& S, int env, int p0) {
+  const int lane = threadIdx.x & 63;
+  const ScenarioParams sp = scenario_params<DYN, NT>(P, S);
+  if (P.rng == LSM_RNG_PHILOX) {
+    GAS uint32_t* rw = gptr(P.s.mt) + (size_t)env * MT_WORDS + MT_N;
+    const uint32_t ridx = *rw - (uint32_t)MT_N;
+    PhiloxView v;
+    v.key = (uint32_t)(P.seed + 1000 * (P.env_offset + env));
+    v.ridx = ridx;
+    v.avail = 1 << 30;
+    random_scenario_wave(v, sp, S.ps, S.lm, S.scen);
+    esync<64>();
+    if (lane == 0) *rw = ridx + 1 + (uint32_t)MT_N;
+    return;
+  }
+  MtView v;
+  v.key = S.mt;
+  v.nxt = S.mtn;
+  v.p0 = p0;
+  v.avail = min(2 * MT_N - p0, P.mt_stage);
+  const int used = random_scenario_wave(v, sp, S.ps, S.lm, S.scen);
+  esync<64>();
+  if (lane == 0) S.mt[MT_N] = used > v.avail ? MT_OVER : (uint32_t)(p0 + used);
+  esync<64>();
 }
 
 // env wave: the stream's new state to HBM (a redraw if the lane ran out), then reset_tail
@@ -476,11 +678,15 @@ void rollout_team_kernel(const KParams* __restrict__ Pp, const KStep K) {
     int p0 = 0;
     if (rs) p0 = team_reset_prep<DYN, NT>(P, S, env, K.cur_new);
     TSTAMP(19);
+#ifdef LSM_AB_WDRAW
+    if (rs) team_scenario_wave<DYN, NT>(P, S, env, p0);
+#else
     __syncthreads();
     // (each env's wave drawing its own env on one lane measured slower: reset steps 85.7-89.1 vs
     // 79.8-85.9 us, profiles/r03_v19_reset_*.json)
     if (w == 0 && lane < G && team_rs[lane]) team_scenario<DYN, NT>(P, smem, B, lane, env0 + lane);
     __syncthreads();
+#endif
     TSTAMP(20);
     if (rs) {
       team_reset_finish<DYN, NT>(P, S, env, p0);
