@@ -211,6 +211,10 @@ struct KStep {
   const float4* rec;      // StateDev::rec and its strides, in the arguments so the first loads of a
   uint32_t rec_stride16, rec16, a2_16;   // launch need no dependent load of KParams
   int action_kind, mode, emit_edges, stop_after;   // mode 0 = step, 1 = reset all, 2 = reset from layout
+  // multi-round launches (more workgroups than fit at once): workgroups [stg_lo, stg_hi) of the
+  // first round start stg_ticks (100 MHz realtime ticks) late, so that the rounds that follow
+  // alternate between gather-heavy and store-heavy halves instead of all phases in lockstep
+  uint32_t stg_ticks, stg_lo, stg_hi;
   double cur_new[NCUR];
 };
 
@@ -1018,13 +1022,25 @@ __device__ __forceinline__ void magnetic_partials_wave(const KParams& P, const L
       const double Ly = nr * P.mag_c[k], Lz = nr * P.mag_s[k];
       const double dLy = radius * P.mag_s[k], dLz = nr * P.mag_c[k];
       const double r0 = x - 0.0, r1 = y - Ly, r2 = 0.0 - Lz;
+      const double c0 = dLy * r2 - dLz * r1;
+      const double c1 = dLz * r0 - 0.0 * r2;
+#ifdef LSM_AB_MAGDIV   // round 3: sqrt, rn**3, two float64 divisions per segment
       const double rn = blas_norm3(r0, r1, r2);
       const double sq = rn * rn;
       const double r3 = fma(sq, rn, fma(rn, rn, -sq) * rn);   // rn**3, ~correctly rounded
-      const double c0 = dLy * r2 - dLz * r1;
-      const double c1 = dLz * r0 - 0.0 * r2;
       m0 += c0 / r3;
       m1 += c1 / r3;
+#else
+      // 1 / |r|**3 from v_rsq_f64 (~2^-23 relative) and two Newton steps (~1 ulp), then two
+      // multiplies: a few ulp per term instead of ~1.5, no division (|r| > 0: r0 = x != 0)
+      const double sq = fma(r2, r2, fma(r1, r1, r0 * r0));
+      double ri = __builtin_amdgcn_rsq(sq);
+      ri = fma(0.5 * ri, fma(-sq * ri, ri, 1.0), ri);
+      ri = fma(0.5 * ri, fma(-sq * ri, ri, 1.0), ri);
+      const double i3 = ri * ri * ri;
+      m0 = fma(c0, i3, m0);
+      m1 = fma(c1, i3, m1);
+#endif
     }
   }
   part[lane] = m0;
@@ -1943,6 +1959,39 @@ __device__ __forceinline__ void summary(const KParams& P, const Lds& S, double* 
   if (out[6] == INFINITY) out[6] = P.coord_range;
 }
 
+// summary() with output k on lane k < 8: every lane runs the same pairwise sum over its own source
+// (a per-lane LDS address; the two ratio outputs divide by travel time, the others by 1.0, which
+// is exact), so the eight means cost one. Same sums, same order, same bits as summary().
+struct SummaryLaneAcc {
+  const double* src;     // this lane's stats row
+  const int32_t* rp;     // S.rpost (lane 3)
+  const double* tl;      // travel times (the ratio lanes' denominators)
+  int k;
+  __device__ __forceinline__ double operator()(int i) const {
+    double x = k == 3 ? (double)rp[i] : src[i];
+    if (k == 4 || k == 7) x = x / ((tl[i] == 0) ? 1.0 : tl[i]);
+    return x;
+  }
+};
+template <int NT>
+__device__ __forceinline__ double summary_lane(const KParams& P, const Lds& S, int k) {
+  constexpr int DYN = 0;
+  LSM_DIMS;
+  const int kk = k < 8 ? k : 0;
+  // stats row of output kk: tl td dn (rpost) cf md (min) mu
+  const int row = kk < 3 ? kk : (kk == 3 ? 0 : (kk <= 5 ? kk - 1 : kk - 2));
+  SummaryLaneAcc a{S.stats + row * N, S.rpost, S.stats, kk};
+  double out = np_sum_acc(a, N) / (double)N;
+  if (kk == 0) out = P.dt * out;
+  const double* md = S.stats + 4 * N;
+  if (kk == 6) {
+    out = md[0];
+    for (int i = 1; i < N; ++i) out = (md[i] < out) ? md[i] : out;
+  }
+  if ((kk == 5 || kk == 6) && out == INFINITY) out = P.coord_range;
+  return out;
+}
+
 // summary() with its loops kept rolled (workgroup kernel, N up to 64: unrolled, the scheduler
 // hoists every LDS load of the five pairwise sums and the kernel spills). Same arithmetic.
 template <int NT>
@@ -1992,7 +2041,13 @@ __device__ __forceinline__ void reset_head(const KParams& P, Lds& S, int env, co
   const int lane = threadIdx.x & (LPE - 1);
   LSM_DIMS;
   GAS double* prev = gptr(P.s.prev) + (size_t)env * 8;
-  if (lane == 0) {
+  if (LPE >= 8 && LPE <= WAVE) {
+    const double o = summary_lane<NT>(P, S, lane);
+    if (lane < 8) {
+      prev[lane] = o;
+      gptr(P.o.ep_info)[(size_t)env * 8 + lane] = o;
+    }
+  } else if (lane == 0) {
     double outv[8];
     if (LPE == BT) summary_rolled<NT>(P, S, outv); else summary<NT>(P, S, outv);
     for (int k = 0; k < 8; ++k) {
@@ -3202,6 +3257,7 @@ struct lsm_env {
   bool generic_only;   // LSM_GENERIC=1: never use the compile-time-N kernels (tests): 64 (one env per wave), 32 or 16 (2 or 4 envs per wave)
   int team;   // envs per workgroup of the team kernel (lsm_team.h); 0 = rollout_kernel
   bool lean;  // the team kernel's lean LDS layout (airtaxi, N % 4 == 0, E % 4 == 0)
+  uint32_t stagger_ticks;   // KStep::stg_ticks of multi-round team launches (LSM_STAGGER_US)
 };
 
 static int fail(lsm_env* e, const std::string& msg) {
@@ -3252,6 +3308,23 @@ int launch_team_t(lsm_env* e, const KStep& L, size_t env_bytes, hipStream_t st) 
     attr = true;
   }
   const int blocks = (e->cfg.num_envs + G - 1) / G;
+  static int resident = -1;   // workgroups of this kernel resident at once on the device
+  if (resident < 0) {
+    int per_cu = 0, dev = 0, cus = 0;
+    HIPCHK(e, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rollout_team_kernel<DYN, NT, G>, WAVE * G, lds));
+    HIPCHK(e, hipGetDevice(&dev));
+    HIPCHK(e, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    resident = per_cu * cus;
+  }
+  if (L.mode == 0 && e->stagger_ticks && blocks > resident && resident > 1) {
+    KStep K = L;
+    K.stg_ticks = e->stagger_ticks;
+    K.stg_lo = (uint32_t)(resident / 2);
+    K.stg_hi = (uint32_t)resident;
+    hipLaunchKernelGGL((rollout_team_kernel<DYN, NT, G>), dim3(blocks), dim3(WAVE * G), lds, st,
+                       active_params(e), K);
+    return 0;
+  }
   hipLaunchKernelGGL((rollout_team_kernel<DYN, NT, G>), dim3(blocks), dim3(WAVE * G), lds, st,
                      active_params(e), L);
   return 0;
@@ -3514,6 +3587,8 @@ int lsm_create(const lsm_config* cfg, lsm_env** out) {
   // workgroup share one wave for their per-agent phases. LSM_TEAM=0 selects rollout_kernel,
   // LSM_TEAM=G another instantiated G.
   e->team = 0;
+  e->stagger_ticks = 0;
+  if (const char* v = getenv("LSM_STAGGER_US")) e->stagger_ticks = (uint32_t)std::max(0, (int)(100 * atof(v)));
   // the team kernel runs World.step's inner loop once (num_internal_step = 1, the training
   // default, train.sh:35); more inner steps run in rollout_kernel / the workgroup kernel
   if (!e->block && e->lpe == 64 && L == 2 && !e->generic_only && cfg->num_internal_step <= 1) {
@@ -3875,6 +3950,7 @@ static int launch(lsm_env* e, KStep& L, hipStream_t st) {
   L.rec16 = e->s.rec16;
   L.a2_16 = e->s.a2_16;
   L.stop_after = -1;
+  L.stg_ticks = L.stg_lo = L.stg_hi = 0;
 #ifdef LSM_STAMPS
   if (const char* v = getenv("LSM_STOP_AFTER")) L.stop_after = atoi(v);
 #endif

@@ -54,13 +54,15 @@ __host__ __device__ inline size_t team_env_bytes(size_t bytes, int N) {
 #define TRTSTAMP(k) do { } while (0)
 #endif
 
-// ---- resets: the scenario draws of the workgroup's envs, one lane per env -----------------
+// ---- resets: the scenario draws ------------------------------------------------------------
 // random_scenario is a long scalar sequence (rejection loops, atan2, ~120 MT19937 doubles at N =
 // 8) that every lane of an env's wave used to run identically; with all G waves of the 4
 // workgroups of a CU doing so at once, an auto-reset step cost ~2.5 plain steps. Here each env's
 // wave prepares its stream (the rest of the current MT19937 block in LDS plus the next block,
-// generated out of place), then ONE wave runs the draws of every resetting env of the workgroup,
-// lane g for env g, and each env's wave finishes its own reset.
+// generated out of place), then draws its scenario with the draws spread over its lanes
+// (random_scenario_wave, below), and finishes its own reset. (Round 3's shape, one wave drawing
+// every resetting env of the workgroup on lane g for env g -- team_scenario, LaneMT -- stays as
+// the A/B variant LSM_AB_LANEDRAW.)
 
 // The next MT19937 block (HostMT::gen's arithmetic) into nxt, leaving key intact. Cooperative over
 // the env's 64 lanes: element i >= 227 reads nxt[i - 227], so chunks of 64 run in order.
@@ -281,14 +283,135 @@ __device__ int random_scenario_wave(const V& v, const ScenarioParams& p, double*
   return c;
 }
 
+// random_scenario_wave for two landmarks per agent (every configuration the bench and the
+// reference's training runs use): the per-agent pass keeps only what decides the stream position
+// -- goal point 0, the rejection loop of point 1 (64 tries per ballot), the two keep-previous draws,
+// the airtaxi swap -- as wave-uniform values in registers (no LDS writes, no wave barriers), and
+// records each agent's points and speed-draw position on lane i; the headings (atan2), speeds and
+// heading noise of all agents then run at once, agent i on lane i. Same words, same operations.
+template <class V>
+__device__ int random_scenario_wave2(const V& v, const ScenarioParams& p, double* st, double* lm) {
+  const int lane = threadIdx.x & 63;
+  const int N = p.N, NL = 2 * N;
+  const double wsz = p.world_size, cra = p.ratio_airtaxi, cr = p.ratio_scenario;
+  int c = 0;
+  const int per = p.dyn == 0 ? 4 : 8;
+  for (int i = lane; i < N; i += 64) {
+    const int k = c + per * i;
+    if (p.dyn == 0) {
+      const double x = view_uniform(v, k, -0.8 * wsz, 0.8 * wsz);
+      const double y = view_uniform(v, k + 2, -0.8 * wsz, 0.8 * wsz);
+      st[0 * N + i] = x; st[1 * N + i] = y; st[2 * N + i] = 0.0; st[3 * N + i] = 0.0;
+    } else {
+      const double xmin = -0.5 * wsz;
+      const double xmax = 0.25 * wsz * cra + 0.0 * (1 - cra) * wsz;
+      const double y = view_uniform(v, k, -0.5 * wsz, 0.5 * wsz);
+      const double x = view_uniform(v, k + 2, xmin, xmax);
+      const double spd = view_uniform(v, k + 4, p.goal_speed_min, p.goal_speed_max);
+      const double th = view_uniform(v, k + 6, 0.0, p.two_pi);
+      st[0 * N + i] = x; st[1 * N + i] = y; st[2 * N + i] = th; st[3 * N + i] = spd;
+    }
+  }
+  c += per * N;
+  double x0, x1, y0, y1, dmin, dmax;
+  if (p.dyn == 0) {
+    x0 = -0.5 * wsz; x1 = 0.5 * wsz; y0 = -0.5 * wsz; y1 = 0.5 * wsz;
+    dmin = 0.25 * p.coordination_range; dmax = 0.75 * p.coordination_range;
+  } else {
+    const double yw = 0.1 * (1 - cra) + 0.5 * cra;
+    x0 = 0.0; x1 = 0.75 * wsz; y0 = -yw * wsz; y1 = yw * wsz;
+    dmin = 0.5 * p.coordination_range; dmax = p.coordination_range;
+  }
+  double pax = 0.0, pay = 0.0, pbx = 0.0, pby = 0.0;   // the previous agent's goals
+  double max_ = 0.0, may = 0.0, mbx = 0.0, mby = 0.0;  // lane i: agent i's goals
+  int mcs = 0;                                         // lane i: agent i's speed-draw position
+  for (int i = 0; i < N; ++i) {
+    double ax = view_uniform(v, c, x0, x1), ay = view_uniform(v, c + 2, y0, y1);
+    c += 4;
+    int acc = -1;
+    double bx = 0.0, by = 0.0;
+    for (int base = 0; base < 1000 && acc < 0; base += 64) {
+      const int j = base + lane;
+      double x = 0.0, y = 0.0;
+      bool ok = false;
+      if (j < 1000) {
+        x = view_uniform(v, c + 4 * j, x0, x1);
+        y = view_uniform(v, c + 4 * j + 2, y0, y1);
+        const double dx = ax - x, dy = ay - y;
+        const double d = sqrt(dx * dx + dy * dy);
+        ok = (d > dmin && d < dmax) || j == 999;   // the 1000th try is kept whatever it is
+      }
+      const uint64_t m = __ballot(ok);
+      if (m) {
+        const int t = __ffsll((unsigned long long)m) - 1;
+        acc = base + t;
+        bx = __shfl(x, t);
+        by = __shfl(y, t);
+      }
+    }
+    c += 4 * (acc + 1);
+    if (i > 0) {   // the previous agent's goals, each kept with probability 1/2 (a draw each)
+      if (view_uniform(v, c, 0.0, 1.0) < 0.5) { ax = pax; ay = pay; }
+      if (view_uniform(v, c + 2, 0.0, 1.0) < 0.5) { bx = pbx; by = pby; }
+      c += 4;
+    }
+    if (p.dyn != 0 && ax > bx) {
+      const double tx = ax, ty = ay;
+      ax = bx; ay = by;
+      bx = tx; by = ty;
+    }
+    if (lane == i) { max_ = ax; may = ay; mbx = bx; mby = by; mcs = c; }
+    pax = ax; pay = ay; pbx = bx; pby = by;
+    if (p.dyn == 0) c += 2 * 2 + 2;   // L goal speeds and the switch
+    c += 2;                           // heading noise of the one leg
+  }
+  if (lane < N) {
+    const int i = lane;
+    const double h = atan2(mby - may, mbx - max_);
+    double s0, s1;
+    if (p.dyn != 0) {
+      s0 = s1 = p.goal_speed_max * 1.0;
+    } else {
+      const double var = view_uniform(v, mcs + 4, 0.0, 1.0);
+      const bool use_rnd = var < py_min(cr, 1 - 0.2);
+      const double r0 = view_uniform(v, mcs, p.goal_speed_min, p.goal_speed_max);
+      const double r1 = view_uniform(v, mcs + 2, p.goal_speed_min, p.goal_speed_max);
+      s0 = use_rnd ? r0 : p.goal_speed_max * 1.0;
+      s1 = use_rnd ? r1 : p.goal_speed_min;
+    }
+    const double pr = (p.dyn == 0) ? cr * 0.25 * p.pi : cra * 0.1 * p.pi;
+    const double h0 = h + view_uniform(v, mcs + (p.dyn == 0 ? 6 : 0), -pr, pr);
+    lm[0 * NL + i] = max_;     lm[0 * NL + N + i] = mbx;
+    lm[1 * NL + i] = may;      lm[1 * NL + N + i] = mby;
+    lm[2 * NL + i] = h0;       lm[2 * NL + N + i] = h;
+    lm[3 * NL + i] = s0;       lm[3 * NL + N + i] = s1;
+  }
+  return c;
+}
+
 // env wave: summary, curriculum, shift; the MT19937 stream staged in LDS (start pos kept)
 template <int DYN, int NT>
 __device__ __forceinline__ int team_reset_prep(const KParams& P, Lds& S, int env, const double* cur_new) {
   const int lane = threadIdx.x & 63;
-  reset_head<DYN, 64, NT>(P, S, env, cur_new);
-  if (P.rng == LSM_RNG_PHILOX) return 0;
+  // the env's MT19937 state loads are issued first, so their latency overlaps the summary
+  constexpr int MQ = (MT_WORDS + 63) / 64;
+  uint32_t mr[MQ];
+  const bool mt = P.rng != LSM_RNG_PHILOX;
   const GAS uint32_t* mtg = gptr(P.s.mt) + (size_t)env * MT_WORDS;
-  for (int k = lane; k < MT_WORDS; k += 64) S.mt[k] = mtg[k];
+  if (mt) {
+#pragma unroll
+    for (int q = 0; q < MQ; ++q) {
+      const int k = lane + 64 * q;
+      mr[q] = mtg[k < MT_WORDS ? k : 0];
+    }
+  }
+  reset_head<DYN, 64, NT>(P, S, env, cur_new);
+  if (!mt) return 0;
+#pragma unroll
+  for (int q = 0; q < MQ; ++q) {
+    const int k = lane + 64 * q;
+    if (k < MT_WORDS) S.mt[k] = mr[q];
+  }
   esync<64>();
   const int p0 = (int)S.mt[MT_N];
   mt_next_block(S.mt, S.mtn);
@@ -333,7 +456,8 @@ __device__ __forceinline__ void team_scenario_wave(const KParams& P, Lds& S, int
     v.key = (uint32_t)(P.seed + 1000 * (P.env_offset + env));
     v.ridx = ridx;
     v.avail = 1 << 30;
-    random_scenario_wave(v, sp, S.ps, S.lm, S.scen);
+    if (sp.L == 2) random_scenario_wave2(v, sp, S.ps, S.lm);
+    else random_scenario_wave(v, sp, S.ps, S.lm, S.scen);
     esync<64>();
     if (lane == 0) *rw = ridx + 1 + (uint32_t)MT_N;
     return;
@@ -343,7 +467,7 @@ __device__ __forceinline__ void team_scenario_wave(const KParams& P, Lds& S, int
   v.nxt = S.mtn;
   v.p0 = p0;
   v.avail = min(2 * MT_N - p0, P.mt_stage);
-  const int used = random_scenario_wave(v, sp, S.ps, S.lm, S.scen);
+  const int used = sp.L == 2 ? random_scenario_wave2(v, sp, S.ps, S.lm) : random_scenario_wave(v, sp, S.ps, S.lm, S.scen);
   esync<64>();
   if (lane == 0) S.mt[MT_N] = used > v.avail ? MT_OVER : (uint32_t)(p0 + used);
   esync<64>();
@@ -402,6 +526,10 @@ void rollout_team_kernel(const KParams* __restrict__ Pp, const KStep K) {
   const int aenv = env0 + aslot;
   Lds A = carve(smem + (size_t)aslot * B, N, NL, E, F, DYN == 1 && P.lean != 0);
   constexpr int WB = 0, WD = 1 % G;           // agent-phase waves (different SIMDs)
+  if (K.stg_ticks && blockIdx.x >= K.stg_lo && blockIdx.x < K.stg_hi) {   // launch_team_t
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (__builtin_amdgcn_s_memrealtime() - t0 < K.stg_ticks) __builtin_amdgcn_s_sleep(8);
+  }
   TRTSTAMP(13);
   TSTAMP(0);
 #ifdef LSM_STAMPS
@@ -678,12 +806,13 @@ void rollout_team_kernel(const KParams* __restrict__ Pp, const KStep K) {
     int p0 = 0;
     if (rs) p0 = team_reset_prep<DYN, NT>(P, S, env, K.cur_new);
     TSTAMP(19);
-#ifdef LSM_AB_WDRAW
+#ifndef LSM_AB_LANEDRAW
+    // each resetting env's wave draws its own scenario on all 64 lanes (random_scenario_wave):
+    // reset steps 70.0-73.6 us vs 86.4-90.2 with one wave drawing lane g for env g
+    // (profiles/r04_v1_reset_{wdraw,base}.json, config 3)
     if (rs) team_scenario_wave<DYN, NT>(P, S, env, p0);
 #else
     __syncthreads();
-    // (each env's wave drawing its own env on one lane measured slower: reset steps 85.7-89.1 vs
-    // 79.8-85.9 us, profiles/r03_v19_reset_*.json)
     if (w == 0 && lane < G && team_rs[lane]) team_scenario<DYN, NT>(P, smem, B, lane, env0 + lane);
     __syncthreads();
 #endif
