@@ -123,15 +123,23 @@ struct MtView {   // the staged MT19937 blocks (team_reset_prep): current from p
   const uint32_t* key;
   const uint32_t* nxt;
   int p0, avail;   // words available from p0 (lane draws beyond avail are flagged by the caller)
-  __device__ __forceinline__ uint32_t word(int k) const {
+  // one unconditional LDS read from a selected address (a branch per word made every read wait
+  // for the previous one: 3.7 k cycles per agent of the draw instead of ~1 k)
+  __device__ __forceinline__ uint32_t raw(int k) const {
     const int a = p0 + k;
-    const uint32_t y = a < MT_N ? key[a] : (a < 2 * MT_N ? nxt[a - MT_N] : 0u);
-    return mt_temper(y);
+    const bool in = a < 2 * MT_N;
+    const uint32_t* q = a < MT_N ? key + a : nxt + (a - MT_N);
+    const uint32_t y = *(in ? q : key);
+    return in ? y : 0u;
   }
+  __device__ __forceinline__ uint32_t word(int k) const { return mt_temper(raw(k)); }
+  static __device__ __forceinline__ uint32_t tw(uint32_t y) { return mt_temper(y); }
 };
 struct PhiloxView {   // LSM_RNG_PHILOX: word k = element k % 4 of counter block k / 4
   uint32_t key, ridx;
   int avail;
+  __device__ __forceinline__ uint32_t raw(int k) const { return word(k); }
+  static __device__ __forceinline__ uint32_t tw(uint32_t y) { return y; }
   __device__ __forceinline__ uint32_t word(int k) const {
     const uint32_t ctr[4] = {(uint32_t)k >> 2, ridx, 0u, 0u}, kk[2] = {key, 0x4c534d31u};
     uint32_t o[4];
@@ -140,10 +148,23 @@ struct PhiloxView {   // LSM_RNG_PHILOX: word k = element k % 4 of counter block
     return e == 0 ? o[0] : e == 1 ? o[1] : e == 2 ? o[2] : o[3];
   }
 };
+__device__ __forceinline__ double readlane_f64(double x, int l) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(x), l);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(x), l);
+  return __hiloint2double(hi, lo);
+}
+
 // RandomState.uniform(lo, hi) from words k, k + 1 (numpy's random_sample)
 template <class V>
 __device__ __forceinline__ double view_uniform(const V& v, int k, double lo, double hi) {
   const uint32_t a = v.word(k) >> 5, b = v.word(k + 1) >> 6;
+  const double range = hi - lo;
+  return lo + range * ((a * 67108864.0 + b) / 9007199254740992.0);
+}
+// the same from raw (untempered) words already read
+template <class V>
+__device__ __forceinline__ double raw_uniform(uint32_t r0, uint32_t r1, double lo, double hi) {
+  const uint32_t a = V::tw(r0) >> 5, b = V::tw(r1) >> 6;
   const double range = hi - lo;
   return lo + range * ((a * 67108864.0 + b) / 9007199254740992.0);
 }
@@ -284,14 +305,23 @@ __device__ int random_scenario_wave(const V& v, const ScenarioParams& p, double*
 }
 
 // random_scenario_wave for two landmarks per agent (every configuration the bench and the
-// reference's training runs use): the per-agent pass keeps only what decides the stream position
-// -- goal point 0, the rejection loop of point 1 (64 tries per ballot), the two keep-previous draws,
-// the airtaxi swap -- as wave-uniform values in registers (no LDS writes, no wave barriers), and
-// records each agent's points and speed-draw position on lane i; the headings (atan2), speeds and
-// heading noise of all agents then run at once, agent i on lane i. Same words, same operations.
+// reference's training runs use): only the rejection loop's length decides where the next agent's
+// words start, so the agent-by-agent pass resolves just that (64 tries per ballot) and everything
+// else runs for all agents at once, agent i on lane i; no LDS writes, no wave barriers. Same words,
+// same operations, same values as random_scenario.
+#ifdef LSM_STAMPS
+#define DSTAMP(k)                                                                                  \
+  do {                                                                                             \
+    if (stp && lane == 0) stp[k] = __builtin_amdgcn_s_memtime();                                   \
+  } while (0)
+#else
+#define DSTAMP(k) do { } while (0)
+#endif
 template <class V>
-__device__ int random_scenario_wave2(const V& v, const ScenarioParams& p, double* st, double* lm) {
+__device__ int random_scenario_wave2(const V& v, const ScenarioParams& p, double* st, double* lm,
+                                     GAS unsigned long long* stp = nullptr) {
   const int lane = threadIdx.x & 63;
+  (void)stp;
   const int N = p.N, NL = 2 * N;
   const double wsz = p.world_size, cra = p.ratio_airtaxi, cr = p.ratio_scenario;
   int c = 0;
@@ -313,6 +343,7 @@ __device__ int random_scenario_wave2(const V& v, const ScenarioParams& p, double
     }
   }
   c += per * N;
+  DSTAMP(23);
   double x0, x1, y0, y1, dmin, dmax;
   if (p.dyn == 0) {
     x0 = -0.5 * wsz; x1 = 0.5 * wsz; y0 = -0.5 * wsz; y1 = 0.5 * wsz;
@@ -322,49 +353,78 @@ __device__ int random_scenario_wave2(const V& v, const ScenarioParams& p, double
     x0 = 0.0; x1 = 0.75 * wsz; y0 = -yw * wsz; y1 = yw * wsz;
     dmin = 0.5 * p.coordination_range; dmax = p.coordination_range;
   }
-  double pax = 0.0, pay = 0.0, pbx = 0.0, pby = 0.0;   // the previous agent's goals
-  double max_ = 0.0, may = 0.0, mbx = 0.0, mby = 0.0;  // lane i: agent i's goals
-  int mcs = 0;                                         // lane i: agent i's speed-draw position
+  // Agent blocks in stream order: [point 0: 4][tries: 4 (acc + 1)][keep: 4, agents i > 0]
+  // [speeds: 6, DI][noise: 2]; only acc varies. (1) The chain of block starts: per agent, point 0
+  // and 64 tries at once (try j on lane j), the first accepted try by ballot -- nothing else on the
+  // chain; (2) agent i's draws on lane i; (3) the keep-previous / airtaxi-swap chain in agent order
+  // (readlane, uniform); (4) headings, speeds, noise on lane i.
+  const int after = 4 + (p.dyn == 0 ? 6 : 0) + 2;
+  int my_s = 0, my_acc = 0;
   for (int i = 0; i < N; ++i) {
-    double ax = view_uniform(v, c, x0, x1), ay = view_uniform(v, c + 2, y0, y1);
-    c += 4;
+    uint32_t r[8];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) r[q] = v.raw(c + q);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) r[4 + q] = v.raw(c + 4 + 4 * lane + q);
+    const double ax = raw_uniform<V>(r[0], r[1], x0, x1), ay = raw_uniform<V>(r[2], r[3], y0, y1);
     int acc = -1;
-    double bx = 0.0, by = 0.0;
     for (int base = 0; base < 1000 && acc < 0; base += 64) {
       const int j = base + lane;
-      double x = 0.0, y = 0.0;
+      if (base > 0) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) r[4 + q] = v.raw(c + 4 + 4 * j + q);
+      }
       bool ok = false;
       if (j < 1000) {
-        x = view_uniform(v, c + 4 * j, x0, x1);
-        y = view_uniform(v, c + 4 * j + 2, y0, y1);
+        const double x = raw_uniform<V>(r[4], r[5], x0, x1), y = raw_uniform<V>(r[6], r[7], y0, y1);
         const double dx = ax - x, dy = ay - y;
         const double d = sqrt(dx * dx + dy * dy);
         ok = (d > dmin && d < dmax) || j == 999;   // the 1000th try is kept whatever it is
       }
       const uint64_t m = __ballot(ok);
-      if (m) {
-        const int t = __ffsll((unsigned long long)m) - 1;
-        acc = base + t;
-        bx = __shfl(x, t);
-        by = __shfl(y, t);
-      }
+      if (m) acc = base + __ffsll((unsigned long long)m) - 1;
     }
-    c += 4 * (acc + 1);
-    if (i > 0) {   // the previous agent's goals, each kept with probability 1/2 (a draw each)
-      if (view_uniform(v, c, 0.0, 1.0) < 0.5) { ax = pax; ay = pay; }
-      if (view_uniform(v, c + 2, 0.0, 1.0) < 0.5) { bx = pbx; by = pby; }
-      c += 4;
+    if (lane == i) { my_s = c; my_acc = acc; }
+    c += 4 + 4 * (acc + 1) + after - (i == 0 ? 4 : 0);
+  }
+  DSTAMP(24);
+  double dax = 0.0, day = 0.0, dbx = 0.0, dby = 0.0;
+  int kp0 = 0, kp1 = 0, mcs = 0;
+  if (lane < N) {
+    const int t = my_s + 4 + 4 * my_acc;
+    uint32_t r[8];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) r[q] = v.raw(my_s + q);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) r[4 + q] = v.raw(t + q);
+    dax = raw_uniform<V>(r[0], r[1], x0, x1); day = raw_uniform<V>(r[2], r[3], y0, y1);
+    dbx = raw_uniform<V>(r[4], r[5], x0, x1); dby = raw_uniform<V>(r[6], r[7], y0, y1);
+    int k = t + 4;
+    if (lane > 0) {   // the previous agent's goals, each kept with probability 1/2 (a draw each)
+      kp0 = view_uniform(v, k, 0.0, 1.0) < 0.5;
+      kp1 = view_uniform(v, k + 2, 0.0, 1.0) < 0.5;
+      k += 4;
+    }
+    mcs = k;
+  }
+  double pax = 0.0, pay = 0.0, pbx = 0.0, pby = 0.0;   // the previous agent's goals
+  double max_ = 0.0, may = 0.0, mbx = 0.0, mby = 0.0;  // lane i: agent i's goals
+  for (int a = 0; a < N; ++a) {
+    double ax = readlane_f64(dax, a), ay = readlane_f64(day, a);
+    double bx = readlane_f64(dbx, a), by = readlane_f64(dby, a);
+    if (a > 0) {
+      if (__builtin_amdgcn_readlane(kp0, a)) { ax = pax; ay = pay; }
+      if (__builtin_amdgcn_readlane(kp1, a)) { bx = pbx; by = pby; }
     }
     if (p.dyn != 0 && ax > bx) {
       const double tx = ax, ty = ay;
       ax = bx; ay = by;
       bx = tx; by = ty;
     }
-    if (lane == i) { max_ = ax; may = ay; mbx = bx; mby = by; mcs = c; }
+    if (lane == a) { max_ = ax; may = ay; mbx = bx; mby = by; }
     pax = ax; pay = ay; pbx = bx; pby = by;
-    if (p.dyn == 0) c += 2 * 2 + 2;   // L goal speeds and the switch
-    c += 2;                           // heading noise of the one leg
   }
+  DSTAMP(25);
   if (lane < N) {
     const int i = lane;
     const double h = atan2(mby - may, mbx - max_);
@@ -386,8 +446,10 @@ __device__ int random_scenario_wave2(const V& v, const ScenarioParams& p, double
     lm[2 * NL + i] = h0;       lm[2 * NL + N + i] = h;
     lm[3 * NL + i] = s0;       lm[3 * NL + N + i] = s1;
   }
+  DSTAMP(26);
   return c;
 }
+#undef DSTAMP
 
 // env wave: summary, curriculum, shift; the MT19937 stream staged in LDS (start pos kept)
 template <int DYN, int NT>
@@ -467,7 +529,12 @@ __device__ __forceinline__ void team_scenario_wave(const KParams& P, Lds& S, int
   v.nxt = S.mtn;
   v.p0 = p0;
   v.avail = min(2 * MT_N - p0, P.mt_stage);
-  const int used = sp.L == 2 ? random_scenario_wave2(v, sp, S.ps, S.lm) : random_scenario_wave(v, sp, S.ps, S.lm, S.scen);
+#ifdef LSM_STAMPS
+  GAS unsigned long long* stp = gptr(P.stamps) ? gptr(P.stamps) + (size_t)env * LSM_NSTAMP : nullptr;
+#else
+  GAS unsigned long long* stp = nullptr;
+#endif
+  const int used = sp.L == 2 ? random_scenario_wave2(v, sp, S.ps, S.lm, stp) : random_scenario_wave(v, sp, S.ps, S.lm, S.scen);
   esync<64>();
   if (lane == 0) S.mt[MT_N] = used > v.avail ? MT_OVER : (uint32_t)(p0 + used);
   esync<64>();

@@ -102,7 +102,9 @@ def main():
                            ("B integrate", 9, 2), ("D reward", 3, 10),
                            ("D info", 10, 11), ("D rows+stats", 11, 8), ("E info/dones", 4, 18),
                            ("E graph+record", 18, 5), ("R prep", 18, 19), ("R prep->draws", 19, 20),
-                           ("R finish+dist", 20, 21), ("R emit", 21, 22), ("R store", 22, 5)]:
+                           ("R finish+dist", 20, 21), ("R emit", 21, 22), ("R store", 22, 5),
+                           ("R draw: states", 19, 23), ("R draw: blocks+chain", 23, 24),
+                           ("R draw: agents+keep", 24, 25), ("R draw: tail", 25, 26), ("R draw->20", 26, 20)]:
             v = ag[:, j] - ag[:, i]
             v = v[(ag[:, i] != 0) & (ag[:, j] != 0)]
             print("%-18s %12.0f   (agent-wave rows: %d)" % (name, np.median(v), len(v)))
