@@ -1024,15 +1024,10 @@ __device__ __forceinline__ void magnetic_partials_wave(const KParams& P, const L
       const double r0 = x - 0.0, r1 = y - Ly, r2 = 0.0 - Lz;
       const double c0 = dLy * r2 - dLz * r1;
       const double c1 = dLz * r0 - 0.0 * r2;
-#ifdef LSM_AB_MAGDIV   // round 3: sqrt, rn**3, two float64 divisions per segment
-      const double rn = blas_norm3(r0, r1, r2);
-      const double sq = rn * rn;
-      const double r3 = fma(sq, rn, fma(rn, rn, -sq) * rn);   // rn**3, ~correctly rounded
-      m0 += c0 / r3;
-      m1 += c1 / r3;
-#else
       // 1 / |r|**3 from v_rsq_f64 (~2^-23 relative) and two Newton steps (~1 ulp), then two
-      // multiplies: a few ulp per term instead of ~1.5, no division (|r| > 0: r0 = x != 0)
+      // multiplies: a few ulp per term instead of ~1.5, no division (|r| > 0: r0 = x != 0).
+      // Round 3 took sqrt, rn**3 and two float64 divisions: 33.08 vs 31.82 us per step at config 2
+      // (profiles/r04_v2_ab_c2_mag.txt).
       const double sq = fma(r2, r2, fma(r1, r1, r0 * r0));
       double ri = __builtin_amdgcn_rsq(sq);
       ri = fma(0.5 * ri, fma(-sq * ri, ri, 1.0), ri);
@@ -1040,7 +1035,6 @@ __device__ __forceinline__ void magnetic_partials_wave(const KParams& P, const L
       const double i3 = ri * ri * ri;
       m0 = fma(c0, i3, m0);
       m1 = fma(c1, i3, m1);
-#endif
     }
   }
   part[lane] = m0;
@@ -1636,11 +1630,10 @@ __device__ __forceinline__ void emit_adj_uniform(const KParams& P, const Lds& S,
 template <int DYN, int LPE, int NT>
 __device__ __forceinline__ void emit_nodes(const KParams& P, Lds& S, int env, bool uni);
 
-// `adj_done` / `nodes_done`: the uniform adjacency / node_obs were already stored (speculatively,
-// earlier in the step); they are rewritten here only if an agent changed status.
+// `adj_done`: the uniform adjacency was already stored (speculatively, in phase D of the team
+// kernel); it is rewritten here only if an agent changed status.
 template <int DYN, int LPE, int NT>
-__device__ __forceinline__ void emit_graph(const KParams& P, Lds& S, int env, bool adj_done = false,
-                                           bool nodes_done = false) {
+__device__ __forceinline__ void emit_graph(const KParams& P, Lds& S, int env, bool adj_done = false) {
   const int lane = threadIdx.x & (LPE - 1);
   LSM_DIMS;
   // No agent changed done / reached status this step (the common case): every ego then has
@@ -1648,7 +1641,6 @@ __device__ __forceinline__ void emit_graph(const KParams& P, Lds& S, int env, bo
   // its output words once and stores them for all N egos.
   const bool uni = !S.dep0 &&
                    group_all<LPE>(lane >= N || (S.dpre[lane] == S.dpost[lane] && S.rpre[lane] == S.rpost[lane]));
-  if (uni && adj_done && nodes_done) return;
   if (DYN == 0) build_rows_di<LPE, NT>(P, S); else trig_table_at<LPE, NT>(P, S);
   esync<LPE>();
   // ---- adjacency: ego e, row r, col c ------------------------------------------------------
@@ -1713,7 +1705,7 @@ __device__ __forceinline__ void emit_graph(const KParams& P, Lds& S, int env, bo
       adj_out[q] = (((m >> r) | (m >> c)) & 1ull) ? 0.0f : fv1(S, N, NL, E, r, c);
     }
   }
-  if (!(uni && nodes_done)) emit_nodes<DYN, LPE, NT>(P, S, env, uni);
+  emit_nodes<DYN, LPE, NT>(P, S, env, uni);
 }
 
 // node_obs [N][E][F] of one env (DI rows / airtaxi trig table already in LDS). `uni`: no

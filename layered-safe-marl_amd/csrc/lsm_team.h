@@ -61,8 +61,7 @@ __host__ __device__ inline size_t team_env_bytes(size_t bytes, int N) {
 // wave prepares its stream (the rest of the current MT19937 block in LDS plus the next block,
 // generated out of place), then draws its scenario with the draws spread over its lanes
 // (random_scenario_wave, below), and finishes its own reset. (Round 3's shape, one wave drawing
-// every resetting env of the workgroup on lane g for env g -- team_scenario, LaneMT -- stays as
-// the A/B variant LSM_AB_LANEDRAW.)
+// every resetting env of the workgroup on lane g for env g, measured slower and was removed.)
 
 // The next MT19937 block (HostMT::gen's arithmetic) into nxt, leaving key intact. Cooperative over
 // the env's 64 lanes: element i >= 227 reads nxt[i - 227], so chunks of 64 run in order.
@@ -79,36 +78,9 @@ __device__ __forceinline__ void mt_next_block(const uint32_t* key, uint32_t* nxt
   esync<64>();
 }
 
-// One env's numpy stream for a lane that draws that env's scenario alone: the current block
-// from pos on, then the next block. A scenario needing more (over 624 words beyond the current
-// block, or past `lim`: KParams::mt_stage, LSM_MT_STAGE, which tests lower to exercise this path)
-// sets `over` and stops the draw (the rejection loops check exhausted()); the env's wave then
-// redraws it with the cooperative stream.
+// S.mt[MT_N] after a draw that ran past the staged stream (the env's wave then redraws it with the
+// cooperative stream, team_reset_finish)
 constexpr uint32_t MT_OVER = 0xffffffffu;
-struct LaneMT {
-  const uint32_t* key;
-  const uint32_t* nxt;
-  int pos;
-  int lim;   // first position not served (<= 2 MT_N)
-  bool over;
-  __device__ __forceinline__ uint32_t next32() {
-    uint32_t y = 0;
-    if (pos >= lim) over = true;
-    else if (pos < MT_N) y = key[pos];
-    else y = nxt[pos - MT_N];
-    ++pos;
-    return mt_temper(y);
-  }
-  __device__ __forceinline__ bool exhausted() const { return over; }
-  __device__ __forceinline__ double next_double() {
-    const uint32_t a = next32() >> 5, b = next32() >> 6;
-    return (a * 67108864.0 + b) / 9007199254740992.0;
-  }
-  __device__ __forceinline__ double uniform(double lo, double hi) {
-    const double range = hi - lo;
-    return lo + range * next_double();
-  }
-};
 
 // ---- the scenario draw on a whole wave (one env per wave) -----------------------------------
 // random_scenario (lsm_scenario.h) consumes its stream strictly in order, but only its rejection
@@ -480,31 +452,6 @@ __device__ __forceinline__ int team_reset_prep(const KParams& P, Lds& S, int env
   return p0;
 }
 
-// lane g of one wave: env g's scenario (its LDS block at smem + g * B)
-template <int DYN, int NT>
-__device__ __forceinline__ void team_scenario(const KParams& P, unsigned char* smem, uint32_t B, int g, int env) {
-  LSM_DIMS;
-  Lds S = carve(smem + (size_t)g * B, N, NL, E, F, DYN == 1 && P.lean != 0);
-  const ScenarioParams sp = scenario_params<DYN, NT>(P, S);
-  if (P.rng == LSM_RNG_PHILOX) {
-    GAS uint32_t* rw = gptr(P.s.mt) + (size_t)env * MT_WORDS + MT_N;
-    const uint32_t ridx = *rw - (uint32_t)MT_N;
-    Philox rng;
-    rng.init((uint32_t)(P.seed + 1000 * (P.env_offset + env)), ridx);
-    random_scenario(rng, sp, S.ps, S.lm, S.scen);
-    *rw = ridx + 1 + (uint32_t)MT_N;
-    return;
-  }
-  LaneMT rng;
-  rng.key = S.mt;
-  rng.nxt = S.mtn;
-  rng.pos = (int)S.mt[MT_N];
-  rng.lim = min(2 * MT_N, rng.pos + P.mt_stage);
-  rng.over = false;
-  random_scenario(rng, sp, S.ps, S.lm, S.scen);
-  S.mt[MT_N] = rng.over ? MT_OVER : (uint32_t)rng.pos;
-}
-
 // env wave: its own env's scenario on the whole wave (random_scenario_wave), from the staged
 // MT19937 blocks (or the Philox stream); S.mt[MT_N] = the new position, MT_OVER if it ran out
 template <int DYN, int NT>
@@ -616,19 +563,6 @@ void rollout_team_kernel(const KParams* __restrict__ Pp, const KStep K) {
   int cstep = 0;
   bool filter_on = false;
   if (live) {
-#ifdef LSM_AB_PRO
-    // the record's loads first, into registers, from the address in the kernel arguments (no
-    // dependent load of the device-resident KParams): the action / pair-word loads issued after
-    // them are younger, so waiting for the record does not wait for them (vmcnt counts in order)
-    const int n16 = split ? (int)K.a2_16 : (int)K.rec16;
-    const GAS f32x4* rsrc = (const GAS f32x4*)K.rec + (size_t)env * K.rec_stride16;
-    f32x4 rr[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int k = lane + q * LPE;
-      if (q * LPE < n16) rr[q] = rsrc[k < n16 ? k : n16 - 1];
-    }
-#endif
     if (K.mode == 0 && lane < N) act = read_action(K, env, N, lane);
     if (PRE) {
 #pragma unroll
@@ -639,16 +573,8 @@ void rollout_team_kernel(const KParams* __restrict__ Pp, const KStep K) {
     }
     // a plain step needs [0, a2) of the record before its distances; the rest (statistics,
     // landmarks) comes in phase B (cold_loads). Resets and the edge output read it all here.
-#ifdef LSM_AB_PRO
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int k = lane + q * LPE;
-      if (q * LPE < n16 && k < n16) ((f32x4*)lbase)[k] = rr[q];
-    }
-#else
     rec_copy<LPE>((const GAS f32x4*)gptr(P.s.rec) + (size_t)env * P.s.rec_stride16, (f32x4*)lbase,
                   split ? P.s.a2_16 : P.s.rec16);
-#endif
     esync<LPE>();
     TSTAMP(12);
     if (lane < N) {
@@ -754,23 +680,8 @@ void rollout_team_kernel(const KParams* __restrict__ Pp, const KStep K) {
   // the speculative adjacency stores of phase D are skipped for an env that auto-resets at the
   // episode-length boundary (known from the step count): the reset emits its outputs instead
   const bool chunked = (E & 3) == 0 && !P.adj_compact && !(P.auto_reset && cstep >= P.episode_length);
-#if defined(LSM_AB_NODEC) || defined(LSM_AB_NODEC0)
-  const bool nodes_c = DYN == 0 && ((E * F) & 3) == 0 && !(P.auto_reset && cstep >= P.episode_length);
-#else
-  constexpr bool nodes_c = false;
-#endif
   uint64_t m_pre = 0;
   if (live) {
-#ifdef LSM_AB_NODEC0
-    // the env's node_obs first thing in C (they need only the integrated positions), speculatively
-    // as below
-    if (nodes_c) {
-      build_rows_di<LPE, NT>(P, S);
-      esync<LPE>();
-      emit_nodes_uniform_di<LPE, NT>(P, S, env, 0, N);
-      esync<LPE>();
-    }
-#endif
     compute_dist<LPE, NT>(P, S, PRE ? prw : nullptr);
     if (P.o.cforce && lane < N) {
       double fx, fy;
@@ -779,16 +690,6 @@ void rollout_team_kernel(const KParams* __restrict__ Pp, const KStep K) {
       cf[0] = fx;
       cf[1] = fy;
     }
-#ifdef LSM_AB_NODEC
-    // the env's node_obs, speculatively: no agent has changed status yet (dpost == dpre here), so
-    // these are the step's rows unless phase D changes one -- phase E then re-emits everything
-    if (nodes_c) {
-      build_rows_di<LPE, NT>(P, S);
-      esync<LPE>();
-      emit_nodes_uniform_di<LPE, NT>(P, S, env, 0, N);
-      esync<LPE>();   // U2 rows read before the magnetic partials overwrite them
-    }
-#endif
     // the magnetic-field segment sums (partials in U2, read by the agent wave in D, before the
     // info rows reuse U2)
     if (DYN == 0 && !P.use_filter_arg) magnetic_partials_wave<LPE, NT>(P, S, S.dpair);
@@ -858,7 +759,7 @@ void rollout_team_kernel(const KParams* __restrict__ Pp, const KStep K) {
     if (!rs) {
       // adjacency already stored in D except WD's (emit_graph rewrites it if a status changed)
 #ifndef LSM_XP_NOOUT
-      emit_graph<DYN, LPE, NT>(P, S, env, chunked && w != WD, nodes_c);
+      emit_graph<DYN, LPE, NT>(P, S, env, chunked && w != WD);
 #endif
       esync<LPE>();
       store_state<DYN, LPE, NT>(P, S, lbase, env, false);
@@ -873,16 +774,10 @@ void rollout_team_kernel(const KParams* __restrict__ Pp, const KStep K) {
     int p0 = 0;
     if (rs) p0 = team_reset_prep<DYN, NT>(P, S, env, K.cur_new);
     TSTAMP(19);
-#ifndef LSM_AB_LANEDRAW
     // each resetting env's wave draws its own scenario on all 64 lanes (random_scenario_wave):
-    // reset steps 70.0-73.6 us vs 86.4-90.2 with one wave drawing lane g for env g
-    // (profiles/r04_v1_reset_{wdraw,base}.json, config 3)
+    // reset steps 70.0-73.6 us vs 86.4-90.2 with round 3's one wave drawing lane g for env g
+    // (profiles/r04_v1_reset_wdraw.json, r04_v2_reset_lanedraw.json, config 3)
     if (rs) team_scenario_wave<DYN, NT>(P, S, env, p0);
-#else
-    __syncthreads();
-    if (w == 0 && lane < G && team_rs[lane]) team_scenario<DYN, NT>(P, smem, B, lane, env0 + lane);
-    __syncthreads();
-#endif
     TSTAMP(20);
     if (rs) {
       team_reset_finish<DYN, NT>(P, S, env, p0);

@@ -685,12 +685,12 @@ def test_gpu_collision_forces_reported_never_applied(kernel, monkeypatch):
 @pytest.mark.parametrize("team", ["4", "2", "8", "4s"])
 @pytest.mark.parametrize("dyn,N", [("double_integrator", 8), ("airtaxi", 16)])
 def test_gpu_team_kernel_resets_match_oracle(dyn, N, team, monkeypatch):
-    """The team kernel's auto-resets (all of a workgroup's envs, or some, reset in one launch; the
-    scenario draws run one lane per env from the staged MT19937 stream, crossing block boundaries
-    over successive resets) against the oracle: 10-step episodes, 75 steps (7 resets per env),
-    envs driven all-done early at different steps so resets do not line up, every output. "4s":
-    the lane streams hold only 40 words (LSM_MT_STAGE), so every draw runs out and takes the
-    cooperative redraw, whose stream state goes back to HBM."""
+    """The team kernel's auto-resets (all of a workgroup's envs, or some, reset in one launch; each
+    resetting env's wave draws its scenario with the agents in parallel from the staged MT19937
+    stream, crossing block boundaries over successive resets) against the oracle: 10-step episodes,
+    75 steps (7 resets per env), envs driven all-done early at different steps so resets do not line
+    up, every output. "4s": the staged stream serves only 40 words (LSM_MT_STAGE), so every draw runs
+    out and takes the cooperative redraw, whose stream state goes back to HBM."""
     import torch
     if dyn == "airtaxi" and team == "8":
         pytest.skip("8 airtaxi envs of 16 agents do not fit one 64-lane agent wave")
