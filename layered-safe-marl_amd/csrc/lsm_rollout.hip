@@ -211,10 +211,6 @@ struct KStep {
   const float4* rec;      // StateDev::rec and its strides, in the arguments so the first loads of a
   uint32_t rec_stride16, rec16, a2_16;   // launch need no dependent load of KParams
   int action_kind, mode, emit_edges, stop_after;   // mode 0 = step, 1 = reset all, 2 = reset from layout
-  // multi-round launches (more workgroups than fit at once): workgroups [stg_lo, stg_hi) of the
-  // first round start stg_ticks (100 MHz realtime ticks) late, so that the rounds that follow
-  // alternate between gather-heavy and store-heavy halves instead of all phases in lockstep
-  uint32_t stg_ticks, stg_lo, stg_hi;
   double cur_new[NCUR];
 };
 
@@ -3249,7 +3245,6 @@ struct lsm_env {
   bool generic_only;   // LSM_GENERIC=1: never use the compile-time-N kernels (tests): 64 (one env per wave), 32 or 16 (2 or 4 envs per wave)
   int team;   // envs per workgroup of the team kernel (lsm_team.h); 0 = rollout_kernel
   bool lean;  // the team kernel's lean LDS layout (airtaxi, N % 4 == 0, E % 4 == 0)
-  uint32_t stagger_ticks;   // KStep::stg_ticks of multi-round team launches (LSM_STAGGER_US)
 };
 
 static int fail(lsm_env* e, const std::string& msg) {
@@ -3300,23 +3295,6 @@ int launch_team_t(lsm_env* e, const KStep& L, size_t env_bytes, hipStream_t st) 
     attr = true;
   }
   const int blocks = (e->cfg.num_envs + G - 1) / G;
-  static int resident = -1;   // workgroups of this kernel resident at once on the device
-  if (resident < 0) {
-    int per_cu = 0, dev = 0, cus = 0;
-    HIPCHK(e, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rollout_team_kernel<DYN, NT, G>, WAVE * G, lds));
-    HIPCHK(e, hipGetDevice(&dev));
-    HIPCHK(e, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    resident = per_cu * cus;
-  }
-  if (L.mode == 0 && e->stagger_ticks && blocks > resident && resident > 1) {
-    KStep K = L;
-    K.stg_ticks = e->stagger_ticks;
-    K.stg_lo = (uint32_t)(resident / 2);
-    K.stg_hi = (uint32_t)resident;
-    hipLaunchKernelGGL((rollout_team_kernel<DYN, NT, G>), dim3(blocks), dim3(WAVE * G), lds, st,
-                       active_params(e), K);
-    return 0;
-  }
   hipLaunchKernelGGL((rollout_team_kernel<DYN, NT, G>), dim3(blocks), dim3(WAVE * G), lds, st,
                      active_params(e), L);
   return 0;
@@ -3579,8 +3557,6 @@ int lsm_create(const lsm_config* cfg, lsm_env** out) {
   // workgroup share one wave for their per-agent phases. LSM_TEAM=0 selects rollout_kernel,
   // LSM_TEAM=G another instantiated G.
   e->team = 0;
-  e->stagger_ticks = 0;
-  if (const char* v = getenv("LSM_STAGGER_US")) e->stagger_ticks = (uint32_t)std::max(0, (int)(100 * atof(v)));
   // the team kernel runs World.step's inner loop once (num_internal_step = 1, the training
   // default, train.sh:35); more inner steps run in rollout_kernel / the workgroup kernel
   if (!e->block && e->lpe == 64 && L == 2 && !e->generic_only && cfg->num_internal_step <= 1) {
@@ -3942,7 +3918,6 @@ static int launch(lsm_env* e, KStep& L, hipStream_t st) {
   L.rec16 = e->s.rec16;
   L.a2_16 = e->s.a2_16;
   L.stop_after = -1;
-  L.stg_ticks = L.stg_lo = L.stg_hi = 0;
 #ifdef LSM_STAMPS
   if (const char* v = getenv("LSM_STOP_AFTER")) L.stop_after = atoi(v);
 #endif

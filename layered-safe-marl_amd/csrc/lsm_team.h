@@ -540,10 +540,6 @@ void rollout_team_kernel(const KParams* __restrict__ Pp, const KStep K) {
   const int aenv = env0 + aslot;
   Lds A = carve(smem + (size_t)aslot * B, N, NL, E, F, DYN == 1 && P.lean != 0);
   constexpr int WB = 0, WD = 1 % G;           // agent-phase waves (different SIMDs)
-  if (K.stg_ticks && blockIdx.x >= K.stg_lo && blockIdx.x < K.stg_hi) {   // launch_team_t
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    while (__builtin_amdgcn_s_memrealtime() - t0 < K.stg_ticks) __builtin_amdgcn_s_sleep(8);
-  }
   TRTSTAMP(13);
   TSTAMP(0);
 #ifdef LSM_STAMPS
