@@ -98,15 +98,16 @@ def table_dict(t):
                 ttr_max=t.ttr_max)
 
 
-def load_traffic(config, n_envs):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary of the same workload."""
+def load_traffic(config, n_envs, build_id):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary of the same workload, and only
+    if it was collected on this library build (lsm_build_id); None otherwise."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(p):
         return None
     try:
         d = json.load(open(p))
         e = d.get("config%d" % config)
-        if e and int(e.get("num_envs", -1)) == n_envs:
+        if e and int(e.get("num_envs", -1)) == n_envs and e.get("build_id") == build_id:
             return float(e["hbm_bytes_per_launch"])
     except Exception:
         return None
@@ -390,7 +391,8 @@ def main():
     sb = step_bytes(N, 2, c["dynamics_type"], c["use_safety_filter"], layout)
     bytes_launch = sb["hbm_bytes"] * n_envs
     achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
-    traffic = load_traffic(a.config, n_envs)
+    build_id = env.lib.lsm_build_id().decode()
+    traffic = load_traffic(a.config, n_envs, build_id)
     resets = int((pre + a.steps) // epl - pre // epl)
     if rank == 0:
         line = {
@@ -413,8 +415,8 @@ def main():
             "ranks": {"rccl_world_size": (dist.get_world_size() if world > 1 else 1), "ms_per_step": per_rank,
                       "env_offsets": offsets, "backend": a.dist_backend if world > 1 else None},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
-                         "frac": achieved / PEAK_HBM_GBPS, "traffic": traffic, "traffic_unit": "HBM bytes/launch (rocprofv3 PMC)",
-                         "kernel": env.kernel_name,
+                         "frac": achieved / PEAK_HBM_GBPS, "traffic": traffic, "traffic_unit": "HBM bytes/launch (rocprofv3 PMC of this build_id; null if none)",
+                         "kernel": env.kernel_name, "build_id": build_id,
                          "kernel_ms": kern_ms, "algorithmic_bytes_per_launch": bytes_launch,
                          "gather_bytes_per_launch": sb["gather_bytes"] * n_envs,
                          "bytes_model": "lsm/perf_model.py: record + outputs + HJ gathers (SURVEY 8(d))"},

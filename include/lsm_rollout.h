@@ -253,6 +253,16 @@ int32_t lsm_action_errors(lsm_env* env, void* hip_stream);
  * library, valid until the next call on the same thread. */
 const char* lsm_kernel_name(const lsm_env* env);
 
+/* Identity of this library's build: the first 16 hex digits of the sha256 of the step kernel's
+ * sources and compiler flags (lsm.build), baked in at compile time. Profiles under profiles/
+ * record it, and bench.py reports PMC traffic only for the build that produced it. */
+const char* lsm_build_id(void);
+
+/* Test-only: the MT19937 words a team-kernel reset may draw from its staged blocks (default 2 MT_N
+ * = 1248; values are clamped to [1, 1248]). A smaller stage makes every draw run out and take the
+ * cooperative redraw (tests/test_gpu_parity.py). Applies from the next launch. */
+int lsm_test_set_mt_stage(lsm_env* env, int32_t words);
+
 /* Shape helpers. */
 int32_t lsm_num_entities(const lsm_env* env);   /* E = N * (1 + L) */
 int32_t lsm_node_features(const lsm_env* env);  /* F */

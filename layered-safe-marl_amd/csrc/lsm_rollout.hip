@@ -180,7 +180,7 @@ struct KParams {
   int rext;          // rbin || collab: rewards finished after every agent's goal / done update
   int use_hj;        // the HJ handle exists (filter on, or LSM_REWARD_HJ_VALUE): resets shift it
   int mt_stage;      // team-kernel resets: MT19937 words one lane may draw from the staged blocks
-                     // (2 MT_N; LSM_MT_STAGE lowers it so tests reach the cooperative redraw)
+                     // (2 MT_N; lsm_test_set_mt_stage lowers it so tests reach the cooperative redraw)
   int64_t seed, env_offset;   // Philox keys: seed + 1000 * (env_offset + env)
   uint32_t lds_dep_off;       // LSM_SCENARIO_DEPARTURES: LDS offset of the departure arrays
   double dt, world_size, coord_range, world_eng, sep_target, max_speed, min_speed, gs_min, gs_max;
@@ -208,8 +208,6 @@ struct KParams {
 struct KStep {
   const void* actions;
   const double* layout;   // mode 2: [n][layout doubles] (lsm_reset_layout)
-  const float4* rec;      // StateDev::rec and its strides, in the arguments so the first loads of a
-  uint32_t rec_stride16, rec16, a2_16;   // launch need no dependent load of KParams
   int action_kind, mode, emit_edges, stop_after;   // mode 0 = step, 1 = reset all, 2 = reset from layout
   double cur_new[NCUR];
 };
@@ -465,7 +463,8 @@ __host__ __device__ inline LdsPlan lds_plan(int N, int NL, int E, int F, bool bl
   p.off[k++] = pb; p.off[k++] = pb + f1; p.off[k++] = pb + f2;
   p.off[k++] = u2; p.off[k++] = u2 + g1; p.off[k++] = u1;   // stage aliases U1 (adj emitted first)
   size_t m = lean ? g2 : (f3 > g2 ? f3 : g2);
-  if (F == 10) m = m > (size_t)(8 * 2 * 64) ? m : (size_t)(8 * 2 * 64);   // magnetic partials (DI, filter off)
+  // magnetic partials + the segment constants (DI, filter off; team kernel: mag_table_store)
+  if (F == 10) m = m > (size_t)(8 * (2 * 64 + 100)) ? m : (size_t)(8 * (2 * 64 + 100));
   m = m > (size_t)(8 * LSM_INFO_FIELDS * N) ? m : (size_t)(8 * LSM_INFO_FIELDS * N);   // info rows
   // the next MT19937 block of a team-kernel reset (live with mt / scen; U2 is free then): after
   // U1's scratch when it fits, else at the U2 base (the team kernels' layouts have room either way,
@@ -786,6 +785,26 @@ __device__ __forceinline__ void interp_grad(const TableDev& T, const double* s, 
   }
 }
 
+// interp_grad with the 2^ND corner gradients of the query's cell already in LDS (lc, gw = 1:
+// the team kernel's speculative prefetch), same weights and summation order
+template <int ND>
+__device__ __forceinline__ void interp_grad_lds(const TableDev& T, const double* s, const f32x4* lc, float* g) {
+  int cell;
+  float w[1 << ND];
+  for (int d = 0; d < ND; ++d) g[d] = 0.0f;
+  if (!grid_cell<ND>(T, s, cell, w)) {
+    for (int d = 0; d < ND; ++d) g[d] = __builtin_nanf("");
+    return;
+  }
+#pragma unroll
+  for (int c = 0; c < (1 << ND); ++c) {
+    const f32x4 a = lc[c];
+    const float gv[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+    for (int d = 0; d < ND; ++d) g[d] = g[d] + w[c] * gv[d];
+  }
+}
+
 // Bounds of the interpolated value at s: the (widened) min / max of the block containing
 // its cell. Same in-range decision and cell index as grid_cell(); false = out of the grid
 // (the lookup is +inf, no load).
@@ -994,8 +1013,36 @@ __device__ __forceinline__ int mag_lanes_per_agent(int N) {
   return G;
 }
 
+// The 50 segment constants (KParams::mag_c then mag_s, 100 contiguous doubles) into an env
+// wave's LDS table: two 8-B loads per lane issued together, one memory round trip. The segment
+// loop used to load mag_c[k] / mag_s[k] from KParams inside each iteration: 7 dependent round
+// trips per lane at N = 8.
+template <int LPE>
+__device__ __forceinline__ void mag_table_issue(const KParams& P, double (&r)[2]) {
+  const int lane = threadIdx.x & (LPE - 1);
+  const GAS double* src = (const GAS double*)gptr(P.mag_c);
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int k = lane + q * LPE;
+    r[q] = src[k < 100 ? k : 0];
+  }
+}
+template <int LPE>
+__device__ __forceinline__ void mag_table_store(const double (&r)[2], double* tab) {
+  const int lane = threadIdx.x & (LPE - 1);
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int k = lane + q * LPE;
+    if (k < 100) tab[k] = r[q];
+  }
+}
+
+// tab: the env's staged constants (mag_table_store; cos at [k], sin at [50 + k]), or nullptr to
+// read KParams directly (one-wave and workgroup kernels). The goal heading's cos / sin are the
+// episode's cached ones (Lds::lmsc: the same functions of the same value, bit for bit).
 template <int LPE, int NT>
-__device__ __forceinline__ void magnetic_partials_wave(const KParams& P, const Lds& S, double* part) {
+__device__ __forceinline__ void magnetic_partials_wave(const KParams& P, const Lds& S, double* part,
+                                                       const double* tab = nullptr) {
   const int lane = threadIdx.x & (LPE - 1);
   constexpr int DYN = 0;
   LSM_DIMS;
@@ -1004,19 +1051,21 @@ __device__ __forceinline__ void magnetic_partials_wave(const KParams& P, const L
   const bool act = a < N;
   const int ai = act ? a : 0;
   const int gi = goal_index(S.rpre[ai], ai, N, NL);
-  const double gx = S.lm[gi], gy = S.lm[NL + gi], gh = S.lm[2 * NL + gi];
+  const double gx = S.lm[gi], gy = S.lm[NL + gi];
+  const double ch = S.lmsc[NL + gi], sh = S.lmsc[gi];
   const double px = S.ps[ai], py = S.ps[N + ai];
-  const double ch = cos(gh), sh = sin(gh);
   double rpx, rpy;
   blas_rot(ch, sh, px - gx, py - gy, rpx, rpy);
   const double radius = 2 * S.cur[C_MDT];
+  const double* mc = tab ? tab : P.mag_c;
+  const double* ms = tab ? tab + 50 : P.mag_s;
   double m0 = 0.0, m1 = 0.0;
   if (act && !(fabs(rpx) < 1e-6)) {
     const double x = 0.5 * rpx, y = rpy;
     const double nr = -radius;
     for (int k = g; k < 50; k += G) {
-      const double Ly = nr * P.mag_c[k], Lz = nr * P.mag_s[k];
-      const double dLy = radius * P.mag_s[k], dLz = nr * P.mag_c[k];
+      const double Ly = nr * mc[k], Lz = nr * ms[k];
+      const double dLy = radius * ms[k], dLz = nr * mc[k];
       const double r0 = x - 0.0, r1 = y - Ly, r2 = 0.0 - Lz;
       const double c0 = dLy * r2 - dLz * r1;
       const double c1 = dLz * r0 - 0.0 * r2;
@@ -1047,13 +1096,41 @@ __device__ __forceinline__ double magnetic_penalty_agent(const KParams& P, const
   double pen = 0.0;
   {
     const int gj = goal_index(S.rpre[i], i, N, NL);
-    const double gxx = S.lm[gj], gyy = S.lm[NL + gj], ghh = S.lm[2 * NL + gj], gs = S.lm[3 * NL + gj];
-    const double c = cos(ghh), s = sin(ghh);
+    const double gxx = S.lm[gj], gyy = S.lm[NL + gj], gs = S.lm[3 * NL + gj];
+    const double c = S.lmsc[NL + gj], s = S.lmsc[gj];   // cos / sin of the goal heading (episode cache)
     double qx, qy, rvx, rvy;
     blas_rot(c, s, S.ps[i] - gxx, S.ps[N + i] - gyy, qx, qy);
     const double dist = blas_norm2(qx, qy);
-    const double polar = atan2(qy, qx);
     blas_rot(c, s, S.ps[2 * N + i] - 0.0, S.ps[3 * N + i] - 0.0, rvx, rvy);
+#ifdef LSM_AB_MAGID
+    // cos / sin of atan2(y, x) as x / |(x, y)|, y / |(x, y)| (ulp-level vs the reference's
+    // np.cos(np.arctan2(..)), inside the reward tolerance); the origin keeps atan2's signed zeros
+    double ch = 1.0, sh = 0.0;
+    if (!(fabs(qx) < 1e-6)) {
+      double s0 = 0.0, s1 = 0.0;
+      for (int q = 0; q < G; ++q) {
+        s0 += part[i * G + q];
+        s1 += part[LPE + i * G + q];
+      }
+      s0 = s0 / 0.5;
+      const double hn = sqrt(s0 * s0 + s1 * s1);
+      if (hn > 0.0 && hn < INFINITY) {
+        ch = s0 / hn;
+        sh = s1 / hn;
+      } else {
+        const double href = atan2(s1, s0);
+        ch = cos(href);
+        sh = sin(href);
+      }
+    }
+    double ref_speed = py_max(gs, 0.1);
+    const double dr = np_clip(dist / 1.5, 0, 1);
+    ref_speed = ref_speed * (1 - dr) + 1.0 * dr;
+    const double rfx = ref_speed * ch, rfy = ref_speed * sh;
+    const double err = blas_norm2(rvx - rfx, rvy - rfy);
+    const double cp = (dist > 0.0 && dist < INFINITY) ? qx / dist : cos(atan2(qy, qx));
+#else
+    const double polar = atan2(qy, qx);
     double href = 0.0;
     if (!(fabs(qx) < 1e-6)) {
       double s0 = 0.0, s1 = 0.0;
@@ -1070,6 +1147,7 @@ __device__ __forceinline__ double magnetic_penalty_agent(const KParams& P, const
     const double rfx = ref_speed * cos(href), rfy = ref_speed * sin(href);
     const double err = blas_norm2(rvx - rfx, rvy - rfy);
     const double cp = cos(polar);
+#endif
     if (cp < P.cos_pi6) {
       pen = err;
     } else {
@@ -1215,8 +1293,11 @@ __device__ __forceinline__ void filter_qp(const KParams& P, const Lds& S, int i,
                                           const double* rel, const float* g, uint8_t& filtered, double& u0,
                                           double& u1);
 
+// gpc / gpj (team kernel, double integrator): the gradient corners prefetched for ego i's partner
+// gpj[i] (the previous step's deconflicting agent), used when the argmin picks that partner
 template <int DYN, int NT>
-__device__ __forceinline__ void filter_prep(const KParams& P, Lds& S, int i) {
+__device__ __forceinline__ void filter_prep(const KParams& P, Lds& S, int i, const f32x4* gpc = nullptr,
+                                            const int* gpj = nullptr) {
   LSM_DIMS;
   float* f = filter_slot(S, N, i);
   int st = 0, jv = -1;
@@ -1232,7 +1313,9 @@ __device__ __forceinline__ void filter_prep(const KParams& P, Lds& S, int i) {
       st = 3;
       double rel[5];
       rel_state<DYN>(S, N, i, jv, rel);
-      if (DYN == 0) interp_grad<4>(P.val, rel, g); else interp_grad<5>(P.val, rel, g);
+      if (DYN == 0 && gpj && gpj[i] == jv) interp_grad_lds<4>(P.val, rel, gpc + 16 * i, g);
+      else if (DYN == 0) interp_grad<4>(P.val, rel, g);
+      else interp_grad<5>(P.val, rel, g);
     }
   }
   float4* f4 = (float4*)f;
@@ -2464,12 +2547,16 @@ __device__ __forceinline__ void collision_force_agent(const Lds& S, int N, int i
   }
 }
 
+// Python / numpy scalar kinds of the reward sums (PyNum, below)
+enum { PY_INT = 0, NP_I64 = 1, NP_F32 = 2, NP_F64 = 3, PY_FLT = 4 };
+
 // Per-agent values of the reward phase that the info phase reuses.
-// `base`: reward_reach_goal's value before the clip, a Python int 0 (base_int) when no float term
-// entered it (the agent was done and got no goal reward); reward_finish adds the optional terms.
+// `base`: reward_reach_goal's value before the clip and its scalar kind (base_kind);
+// reward_finish adds the optional terms.
 struct AgentTmp {
   double rew = 0.0, th_pre = 0.0, spd_pre = 0.0, ct_pre = 1.0, st_pre = 0.0, base = 0.0;
-  bool reached_pre = false, base_int = false;
+  bool reached_pre = false;
+  int base_kind = PY_INT;   // PY_INT, PY_FLT or NP_F64
 };
 
 // obs (before the update), reward, goal / done update of agent i (navigation_graph_safe.py:
@@ -2543,7 +2630,11 @@ __device__ __forceinline__ void reward_agent(const KParams& P, Lds& S, int env, 
     }
   }
   t.base = r;
-  t.base_int = done0 && !(reached && !P.use_masking);
+  // the Python type of reward_reach_goal's `rew` (:692-791): the int 0, np.float64 once a goal reward
+  // or a numpy penalty is added, a Python float after the double integrator's bare `rew -= 1.0`
+  // (filter on, :780) on the int
+  t.base_kind = (reached && (!P.use_masking || !done0)) ? NP_F64 : PY_INT;
+  if (!done0) t.base_kind = (DYN == 0 && P.use_filter_arg) ? (t.base_kind == PY_INT ? PY_FLT : t.base_kind) : NP_F64;
   t.rew = np_clip(r, -40.0, 50.0);
   if (DYN == 1 && S.dep0) {
     // RealisticScenario.update_reached_goal_and_done (navigation_graph_safe.py:1153-1186): the
@@ -2594,8 +2685,8 @@ __device__ __forceinline__ void reward_agent(const KParams& P, Lds& S, int env, 
 // sum is rounded to float32: reward_hj_value's terms are np.float32 (a Python-int weight -- the
 // stair ratio is the int 0 or 1 outside its ramp -- times the JAX float32 value), np.int64 (np.abs
 // of the int 0 that min() returns) or np.float64 (a float64 weight). PyNum restates those
-// promotions (NumPy 2: Python scalars are weak; np.float32 + np.int64 is float64).
-enum { PY_INT = 0, NP_I64 = 1, NP_F32 = 2, NP_F64 = 3 };
+// promotions (NumPy 2, NEP 50: Python int and float scalars are weak -- they take the other
+// operand's numpy type; np.float32 + np.int64 and np.int64 + a Python float are float64).
 struct PyNum {
   double v;
   int t;
@@ -2608,9 +2699,11 @@ __device__ __forceinline__ PyNum py_num(double v, int t) {
 }
 __device__ __forceinline__ PyNum py_add(PyNum a, PyNum b) {
   int t;
+  const bool i64 = a.t == NP_I64 || b.t == NP_I64, pyf = a.t == PY_FLT || b.t == PY_FLT;
   if (a.t == NP_F64 || b.t == NP_F64) t = NP_F64;
-  else if (a.t == NP_F32 || b.t == NP_F32) t = (a.t == NP_I64 || b.t == NP_I64) ? NP_F64 : NP_F32;
-  else t = (a.t == NP_I64 || b.t == NP_I64) ? NP_I64 : PY_INT;
+  else if (a.t == NP_F32 || b.t == NP_F32) t = i64 ? NP_F64 : NP_F32;
+  else if (i64) t = pyf ? NP_F64 : NP_I64;
+  else t = pyf ? PY_FLT : PY_INT;
   return py_num(t == NP_F32 ? (double)((float)a.v + (float)b.v) : a.v + b.v, t);
 }
 
@@ -2706,19 +2799,20 @@ __device__ __forceinline__ void reward_finish(const KParams& P, Lds& S, int env,
       hj = py_add(hj, term);
     }
   }
-  PyNum rew = py_num(t.base, t.base_int ? PY_INT : NP_F64);
+  PyNum rew = py_num(t.base, t.base_kind);
   if (P.rbin & LSM_REWARD_SAFETY_VIOLATION) rew = py_add(rew, sv);
   if (P.rbin & LSM_REWARD_POTENTIAL_CONFLICT)
     rew = py_add(rew, me_cnt > 1 ? py_num(-1.0 * st * me, NP_F64) : py_num(0.0, PY_INT));
   if ((P.rbin & LSM_REWARD_DIFF_FROM_FILTERED_ACTION) && P.use_filter_arg)   // reward_diff_from_filtered_action
     rew = py_add(rew, S.dpre[i] ? py_num(0.0, PY_INT) : py_num(-1.0 * st * S.adiff[i], NP_F64));
   if (P.rbin & LSM_REWARD_HJ_VALUE) rew = py_add(rew, hj);
-  // np.clip(rew, -40, 50): a Python int becomes np.int64; float32 stays float32 (bounds exact)
+  // np.clip(rew, -40, 50): a Python int becomes np.int64, a Python float np.float64; float32 stays
+  // float32 (bounds exact)
   t.rew = np_clip(rew.v, -40.0, 50.0);
   const size_t k = (size_t)env * N + i;
   if (!P.collab) gptr(P.o.rew)[k] = (float)t.rew;
   S.raw[i] = t.rew;
-  S.safe[i] = (double)(rew.t == PY_INT ? NP_I64 : rew.t);
+  S.safe[i] = (double)(rew.t == PY_INT ? NP_I64 : rew.t == PY_FLT ? NP_F64 : rew.t);
 }
 
 // The shared reward (environment.py:1031-1037): np.sum(reward_n) -- the array's dtype is the
@@ -2912,6 +3006,19 @@ __device__ __forceinline__ int read_action(const KStep& K, int env, int N, int i
   return ai;
 }
 
+// t[k] of a 5-entry KParams table for a lane-varying k in [0, 5): the five values are wave-uniform
+// (scalar loads, issued with the launch's other parameter loads) and the lane picks by selects; a
+// vector load t[k] was a memory round trip between the record load and the filter's pair lookups
+__device__ __forceinline__ double sel5(const double* t, int k) {
+  double v[5];
+#pragma unroll
+  for (int q = 0; q < 5; ++q) v[q] = t[q];
+  double r = v[0];
+#pragma unroll
+  for (int q = 1; q < 5; ++q) r = (k == q) ? v[q] : r;
+  return r;
+}
+
 // decode into the env's raw action rows; an index outside Discrete(25) is an error of the
 // caller (the reference's one-hot decode has no such input): flagged for lsm_action_errors(),
 // and the launch kept in bounds
@@ -2919,8 +3026,13 @@ __device__ __forceinline__ void decode_action(const KParams& P, Lds& S, int N, i
   if (ai < 0 || ai > 24) *gptr(P.action_err) = 1;
   const int a = ai < 0 ? 0 : (ai > 24 ? 24 : ai);
   const int xi = a / 5, yi = a - xi * 5;
+#ifdef LSM_AB_DEC
+  S.raw[i] = sel5(P.act0, xi);
+  S.raw[N + i] = sel5(P.act1, yi);
+#else
   S.raw[i] = P.act0[xi];
   S.raw[N + i] = P.act1[yi];
+#endif
 }
 
 // Safety filter of agent i once the pair scratch is filled (core.py:648-677): the filtered
@@ -3212,6 +3324,7 @@ using namespace lsm;
 
 struct lsm_env {
   lsm_config cfg;
+  int mt_stage = 2 * MT_N;   // KParams::mt_stage (lsm_test_set_mt_stage)
   uint16_t* pairs;
   int N, L, NL, E, F, OBS;
   StateDev s;
@@ -3374,8 +3487,7 @@ static void fill_params(const lsm_env* e, KParams& P) {
   P.collab = e->cfg.collaborative ? 1 : 0;
   P.rext = (P.rbin != 0 || P.collab) ? 1 : 0;
   P.use_hj = (e->cfg.use_safety_filter || (e->cfg.reward_terms & LSM_REWARD_HJ_VALUE)) ? 1 : 0;
-  P.mt_stage = 2 * MT_N;
-  if (const char* v = getenv("LSM_MT_STAGE")) P.mt_stage = std::max(1, std::min(2 * MT_N, atoi(v)));
+  P.mt_stage = e->mt_stage;
   P.seed = e->cfg.seed;
   P.env_offset = e->cfg.env_offset;
   P.lds_dep_off = (uint32_t)lds_plan(e->N, e->NL, e->E, e->F, e->block).bytes;
@@ -3844,23 +3956,30 @@ static int check_ready(lsm_env* e, bool stepping) {
 static int sep_check(lsm_env* e, const lsm_curriculum* cur, hipStream_t st) {
   if (!uses_hj(e)) return 0;
   if (cur->separation_distance == e->sep_last) return 0;
-  e->sep_changes++;
-  e->sep_last = cur->separation_distance;
-  const uint32_t need = e->sep_changes > KSEP ? (uint32_t)(e->sep_changes - KSEP) : 0;
-  if (need <= e->s.sepx_cap) return 0;
-  const uint32_t cap = std::max<uint32_t>(std::max<uint32_t>(2 * e->s.sepx_cap, 16), need);
-  const size_t n = (size_t)e->cfg.num_envs;
-  double* nx = nullptr;
-  if (dalloc(e, &nx, n * cap)) return 1;
-  if (e->s.sepx) {
-    HIPCHK(e, hipMemcpy2DAsync(nx, (size_t)cap * 8, e->s.sepx, (size_t)e->s.sepx_cap * 8, (size_t)e->s.sepx_cap * 8,
-                               n, hipMemcpyDeviceToDevice, st));
-    HIPCHK(e, hipStreamSynchronize(st));
-    dfree(e, e->s.sepx);
+  // the overflow rows are grown first; the change is recorded only once they can hold it, so a
+  // failed allocation leaves the handle as it was (a retry grows them again)
+  const int changes = e->sep_changes + 1;
+  const uint32_t need = changes > KSEP ? (uint32_t)(changes - KSEP) : 0;
+  if (need > e->s.sepx_cap) {
+    const uint32_t cap = std::max<uint32_t>(std::max<uint32_t>(2 * e->s.sepx_cap, 16), need);
+    const size_t n = (size_t)e->cfg.num_envs;
+    double* nx = nullptr;
+    if (dalloc(e, &nx, n * cap)) return 1;
+    if (e->s.sepx) {
+      if (hipMemcpy2DAsync(nx, (size_t)cap * 8, e->s.sepx, (size_t)e->s.sepx_cap * 8, (size_t)e->s.sepx_cap * 8, n,
+                           hipMemcpyDeviceToDevice, st) != hipSuccess ||
+          hipStreamSynchronize(st) != hipSuccess) {
+        dfree(e, nx);
+        return fail(e, "growing the HJ separation shift rows failed");
+      }
+      dfree(e, e->s.sepx);
+    }
+    e->s.sepx = nx;
+    e->s.sepx_cap = cap;
+    e->params_dirty = true;
   }
-  e->s.sepx = nx;
-  e->s.sepx_cap = cap;
-  e->params_dirty = true;
+  e->sep_changes = changes;
+  e->sep_last = cur->separation_distance;
   return 0;
 }
 
@@ -3913,10 +4032,6 @@ static int launch(lsm_env* e, KStep& L, hipStream_t st) {
     HIPCHK(e, hipStreamSynchronize(st));
     e->params_dirty = false;
   }
-  L.rec = e->s.rec;
-  L.rec_stride16 = e->s.rec_stride16;
-  L.rec16 = e->s.rec16;
-  L.a2_16 = e->s.a2_16;
   L.stop_after = -1;
 #ifdef LSM_STAMPS
   if (const char* v = getenv("LSM_STOP_AFTER")) L.stop_after = atoi(v);
@@ -3969,6 +4084,18 @@ static int launch(lsm_env* e, KStep& L, hipStream_t st) {
     }
   }
   HIPCHK(e, hipGetLastError());
+  return 0;
+}
+
+#ifndef LSM_BUILD_ID
+#define LSM_BUILD_ID "unknown"
+#endif
+const char* lsm_build_id(void) { return LSM_BUILD_ID; }
+
+int lsm_test_set_mt_stage(lsm_env* e, int32_t words) {
+  if (!e) return 1;
+  e->mt_stage = std::max(1, std::min(2 * MT_N, (int)words));
+  e->params_dirty = true;
   return 0;
 }
 

@@ -49,7 +49,14 @@ __host__ __device__ inline size_t team_env_bytes(size_t bytes, int N) {
   do {                                                                                             \
     if (lane == 0 && live && gptr(P.stamps)) gptr(P.stamps)[(size_t)env * LSM_NSTAMP + (k)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
+// per-phase dynamic instruction counts (lsm.diag_phasecount --team): the launch ends at stop k
+// (launch-uniform; inside A every wave of a workgroup must be live, as at the bench's env counts)
+#define TSTOP(k)                                                                                   \
+  do {                                                                                             \
+    if (K.stop_after == (k)) return;                                                               \
+  } while (0)
 #else
+#define TSTOP(k) do { } while (0)
 #define TSTAMP(k) do { } while (0)
 #define TRTSTAMP(k) do { } while (0)
 #endif
@@ -60,7 +67,7 @@ __host__ __device__ inline size_t team_env_bytes(size_t bytes, int N) {
 // workgroups of a CU doing so at once, an auto-reset step cost ~2.5 plain steps. Here each env's
 // wave prepares its stream (the rest of the current MT19937 block in LDS plus the next block,
 // generated out of place), then draws its scenario with the draws spread over its lanes
-// (random_scenario_wave, below), and finishes its own reset. (Round 3's shape, one wave drawing
+// (random_scenario_wave2, below), and finishes its own reset. (Round 3's shape, one wave drawing
 // every resetting env of the workgroup on lane g for env g, measured slower and was removed.)
 
 // The next MT19937 block (HostMT::gen's arithmetic) into nxt, leaving key intact. Cooperative over
@@ -141,143 +148,10 @@ __device__ __forceinline__ double raw_uniform(uint32_t r0, uint32_t r1, double l
   return lo + range * ((a * 67108864.0 + b) / 9007199254740992.0);
 }
 
-// random_scenario on the 64 lanes of one wave. Returns the words consumed (> v.avail: the staged
-// stream ran out and the caller redraws sequentially). ws: the scenario workspace (SCEN_WS).
-template <class V>
-__device__ int random_scenario_wave(const V& v, const ScenarioParams& p, double* st, double* lm, double* ws) {
-  const int lane = threadIdx.x & 63;
-  const int N = p.N, L = p.L, NL = N * L;
-  const double wsz = p.world_size, cra = p.ratio_airtaxi, cr = p.ratio_scenario;
-  double* gp = ws;                  // [L][2] (lsm_scenario.h's workspace layout)
-  double* prev = ws + 2 * MAX_L;    // [L][2]
-  double* heads = ws + 4 * MAX_L;   // [L]
-  double* speeds = ws + 5 * MAX_L;  // [L]
-  int c = 0;
-  // agent states: a fixed 4 (DI) / 8 (airtaxi) words per agent, agent i on lane i
-  const int per = p.dyn == 0 ? 4 : 8;
-  for (int i = lane; i < N; i += 64) {
-    const int k = c + per * i;
-    if (p.dyn == 0) {
-      const double x = view_uniform(v, k, -0.8 * wsz, 0.8 * wsz);
-      const double y = view_uniform(v, k + 2, -0.8 * wsz, 0.8 * wsz);
-      st[0 * N + i] = x; st[1 * N + i] = y; st[2 * N + i] = 0.0; st[3 * N + i] = 0.0;
-    } else {
-      const double xmin = -0.5 * wsz;
-      const double xmax = 0.25 * wsz * cra + 0.0 * (1 - cra) * wsz;
-      const double y = view_uniform(v, k, -0.5 * wsz, 0.5 * wsz);
-      const double x = view_uniform(v, k + 2, xmin, xmax);
-      const double spd = view_uniform(v, k + 4, p.goal_speed_min, p.goal_speed_max);
-      const double th = view_uniform(v, k + 6, 0.0, p.two_pi);
-      st[0 * N + i] = x; st[1 * N + i] = y; st[2 * N + i] = th; st[3 * N + i] = spd;
-    }
-  }
-  c += per * N;
-  double x0, x1, y0, y1, dmin, dmax;
-  if (p.dyn == 0) {
-    x0 = -0.5 * wsz; x1 = 0.5 * wsz; y0 = -0.5 * wsz; y1 = 0.5 * wsz;
-    dmin = 0.25 * p.coordination_range; dmax = 0.75 * p.coordination_range;
-  } else {
-    const double yw = 0.1 * (1 - cra) + 0.5 * cra;
-    x0 = 0.0; x1 = 0.75 * wsz; y0 = -yw * wsz; y1 = yw * wsz;
-    dmin = 0.5 * p.coordination_range; dmax = p.coordination_range;
-  }
-  for (int i = 0; i < N; ++i) {
-    // separated_positions: point 0, then one rejection loop per further point
-    if (lane == 0) {
-      gp[0] = view_uniform(v, c, x0, x1);
-      gp[1] = view_uniform(v, c + 2, y0, y1);
-    }
-    c += 4;
-    esync<64>();
-    for (int q = 1; q < L; ++q) {
-      int acc = -1;
-      for (int base = 0; base < 1000 && acc < 0; base += 64) {
-        const int j = base + lane;
-        double x = 0.0, y = 0.0;
-        bool ok = false;
-        if (j < 1000) {
-          x = view_uniform(v, c + 4 * j, x0, x1);
-          y = view_uniform(v, c + 4 * j + 2, y0, y1);
-          double d = 0.0;
-          for (int k = 0; k < q; ++k) {
-            const double dx = gp[2 * k] - x, dy = gp[2 * k + 1] - y;
-            const double dk = sqrt(dx * dx + dy * dy);
-            if (k == 0 || dk < d) d = dk;
-          }
-          ok = (d > dmin && d < dmax) || j == 999;   // the 1000th try is kept whatever it is
-        }
-        const uint64_t m = __ballot(ok);
-        if (m) {
-          const int t = __ffsll((unsigned long long)m) - 1;
-          acc = base + t;
-          const double ax = __shfl(x, t), ay = __shfl(y, t);
-          if (lane == 0) {
-            gp[2 * q] = ax;
-            gp[2 * q + 1] = ay;
-          }
-        }
-      }
-      c += 4 * (acc + 1);
-      esync<64>();
-    }
-    // the previous agent's goals, each kept with probability 1/2 (a draw each)
-    if (i > 0) {
-      if (lane < L && view_uniform(v, c + 2 * lane, 0.0, 1.0) < 0.5) {
-        gp[2 * lane] = prev[2 * lane];
-        gp[2 * lane + 1] = prev[2 * lane + 1];
-      }
-      c += 2 * L;
-      esync<64>();
-    }
-    if (lane == 0) {
-      if (p.dyn != 0 && gp[0] > gp[2]) {
-        const double tx = gp[0], ty = gp[1];
-        gp[0] = gp[2]; gp[1] = gp[3];
-        gp[2] = tx; gp[3] = ty;
-      }
-    }
-    esync<64>();
-    if (lane < L - 1) heads[lane] = atan2(gp[2 * lane + 3] - gp[2 * lane + 1], gp[2 * lane + 2] - gp[2 * lane]);
-    // speeds: the double integrator draws L goal speeds and one switch
-    const int cs = c;
-    if (p.dyn == 0) c += 2 * L + 2;
-    esync<64>();
-    const double last = heads[L - 2];
-    if (p.dyn != 0) {
-      if (lane < L) speeds[lane] = p.goal_speed_max * 1.0;
-    } else {
-      const double var = view_uniform(v, cs + 2 * L, 0.0, 1.0);
-      const bool use_rnd = var < py_min(cr, 1 - 0.2);
-      if (lane < L) {
-        const double r = view_uniform(v, cs + 2 * lane, p.goal_speed_min, p.goal_speed_max);
-        double sp = use_rnd ? r : p.goal_speed_max * 1.0;
-        if (!use_rnd && lane == L - 1) sp = p.goal_speed_min;
-        speeds[lane] = sp;
-      }
-    }
-    // heading noise, one draw per leg
-    const double pr = (p.dyn == 0) ? cr * 0.25 * p.pi : cra * 0.1 * p.pi;
-    if (lane < L - 1) heads[lane] += view_uniform(v, c + 2 * lane, -pr, pr);
-    c += 2 * (L - 1);
-    esync<64>();
-    if (lane == 0) heads[L - 1] = last;
-    esync<64>();
-    if (lane < L) {
-      const int idx = lane * N + i;
-      lm[0 * NL + idx] = gp[2 * lane];
-      lm[1 * NL + idx] = gp[2 * lane + 1];
-      lm[2 * NL + idx] = heads[lane];
-      lm[3 * NL + idx] = speeds[lane];
-      prev[2 * lane] = gp[2 * lane];
-      prev[2 * lane + 1] = gp[2 * lane + 1];
-    }
-    esync<64>();
-  }
-  return c;
-}
-
-// random_scenario_wave for two landmarks per agent (every configuration the bench and the
-// reference's training runs use): only the rejection loop's length decides where the next agent's
+// random_scenario (lsm_scenario.h) on the 64 lanes of one wave, for two landmarks per agent (the
+// team kernels run only with L = 2: lsm_create; every configuration the bench and the reference's
+// training runs use). Returns the words consumed (> v.avail: the staged stream ran out and the caller
+// redraws sequentially). Only the rejection loop's length decides where the next agent's
 // words start, so the agent-by-agent pass resolves just that (64 tries per ballot) and everything
 // else runs for all agents at once, agent i on lane i; no LDS writes, no wave barriers. Same words,
 // same operations, same values as random_scenario.
@@ -452,8 +326,9 @@ __device__ __forceinline__ int team_reset_prep(const KParams& P, Lds& S, int env
   return p0;
 }
 
-// env wave: its own env's scenario on the whole wave (random_scenario_wave), from the staged
-// MT19937 blocks (or the Philox stream); S.mt[MT_N] = the new position, MT_OVER if it ran out
+// env wave: its own env's scenario on the whole wave (random_scenario_wave2), from the staged
+// MT19937 blocks (or the Philox stream); S.mt[MT_N] = the new position, MT_OVER if it ran out.
+// L = 2 only (the team kernels' scenario draw, random_scenario_wave2)
 template <int DYN, int NT>
 __device__ __forceinline__ void team_scenario_wave(const KParams& P, Lds& S, int env, int p0) {
   const int lane = threadIdx.x & 63;
@@ -465,8 +340,7 @@ __device__ __forceinline__ void team_scenario_wave(const KParams& P, Lds& S, int
     v.key = (uint32_t)(P.seed + 1000 * (P.env_offset + env));
     v.ridx = ridx;
     v.avail = 1 << 30;
-    if (sp.L == 2) random_scenario_wave2(v, sp, S.ps, S.lm);
-    else random_scenario_wave(v, sp, S.ps, S.lm, S.scen);
+    random_scenario_wave2(v, sp, S.ps, S.lm);
     esync<64>();
     if (lane == 0) *rw = ridx + 1 + (uint32_t)MT_N;
     return;
@@ -481,7 +355,7 @@ __device__ __forceinline__ void team_scenario_wave(const KParams& P, Lds& S, int
 #else
   GAS unsigned long long* stp = nullptr;
 #endif
-  const int used = sp.L == 2 ? random_scenario_wave2(v, sp, S.ps, S.lm, stp) : random_scenario_wave(v, sp, S.ps, S.lm, S.scen);
+  const int used = random_scenario_wave2(v, sp, S.ps, S.lm, stp);
   esync<64>();
   if (lane == 0) S.mt[MT_N] = used > v.avail ? MT_OVER : (uint32_t)(p0 + used);
   esync<64>();
@@ -573,6 +447,7 @@ void rollout_team_kernel(const KParams* __restrict__ Pp, const KStep K) {
                   split ? P.s.a2_16 : P.s.rec16);
     esync<LPE>();
     TSTAMP(12);
+    TSTOP(1);
     if (lane < N) {
       S.dpre[lane] = S.dpost[lane];
       S.rpre[lane] = S.rpost[lane];
@@ -613,6 +488,31 @@ void rollout_team_kernel(const KParams* __restrict__ Pp, const KStep K) {
     if (lane < N) decode_action(P, S, N, lane, act);
     filter_on = S.cur[C_FILT] != 0.0;
     if (filter_on) {
+#ifdef LSM_AB_GPRE
+      // The gradient lookup of each ego at its previous step's deconflicting agent (record decon),
+      // issued with the pair lookups: the argmin picks the same agent in ~99 % of filtered egos, and
+      // then its gradient needs no second memory round trip after the argmin (filter_prep). Lane l
+      // loads corner l % 16 of ego l / 16 (+ 4); parked in U1 (free until the distances).
+      f32x4 gq[2];
+      int gpj[2];
+      if (DYN == 0 && NT == 8) {
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+          const int e = (lane >> 4) + 4 * r, c = lane & 15;
+          int pj = S.decon[e];
+          bool ok = pj >= 0 && pj < N && pj != e && !inactive_pre(S, e) && !inactive_pre(S, pj);
+          int cell = 0;
+          if (ok) {
+            double rel[5];
+            float w[16];
+            rel_state<DYN>(S, N, e, pj, rel);
+            ok = grid_cell<4>(P.val, rel, cell, w);
+          }
+          gpj[r] = ok ? pj : -1;
+          gq[r] = ((const GAS f32x4*)gptr(P.val.gcells))[ok ? (size_t)cell * 16 + c : (size_t)c];
+        }
+      }
+#endif
       const SepChain sc = sep_chain(S.sep, P.s, env);
       for (int p = lane; p < N * N; p += LPE) {
         const int j = p / N, i = p - j * N;   // [j][i]: ego i fastest (bank-conflict-free reads)
@@ -628,14 +528,31 @@ void rollout_team_kernel(const KParams* __restrict__ Pp, const KStep K) {
         S.inr[p] = ok ? 1 : 0;
       }
       TSTAMP(16);
+      TSTOP(2);
       // the deconflicting choice and the HJ gradient lookup of every ego, here where the other
       // waves of the SIMD hide the gather; the agent wave does the QP in B (filter_agent_slot)
+#ifdef LSM_AB_GPRE
+      f32x4* gpc = (f32x4*)S.fval;
+      int* gpi = (int*)(gpc + 16 * NT);
+      if (DYN == 0 && NT == 8) {
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+          const int e = (lane >> 4) + 4 * r;
+          gpc[16 * e + (lane & 15)] = gq[r];
+          if ((lane & 15) == 0) gpi[e] = gpj[r];
+        }
+      }
+      esync<LPE>();
+      if (lane < N) filter_prep<DYN, NT>(P, S, lane, gpc, (DYN == 0 && NT == 8) ? gpi : nullptr);
+#else
       esync<LPE>();
       if (lane < N) filter_prep<DYN, NT>(P, S, lane);
+#endif
       TSTAMP(17);
     }
   }
   TSTAMP(6);
+  TSTOP(3);
   __syncthreads();
   TSTAMP(1);
 
@@ -671,6 +588,7 @@ void rollout_team_kernel(const KParams* __restrict__ Pp, const KStep K) {
   }
   __syncthreads();
   TSTAMP(2);
+  TSTOP(4);
 
   // ---- C. distances; contact forces and magnetic-field sums when asked ------------------------
   // the speculative adjacency stores of phase D are skipped for an env that auto-resets at the
@@ -678,6 +596,11 @@ void rollout_team_kernel(const KParams* __restrict__ Pp, const KStep K) {
   const bool chunked = (E & 3) == 0 && !P.adj_compact && !(P.auto_reset && cstep >= P.episode_length);
   uint64_t m_pre = 0;
   if (live) {
+    // filter off: the magnetic field's segment constants, loaded while the distances are computed
+    // and staged in U2 behind the partial sums (U2 holds no pair matrices without the filter)
+    const bool mag = DYN == 0 && !P.use_filter_arg;
+    double mr[2] = {0.0, 0.0};
+    if (mag) mag_table_issue<LPE>(P, mr);
     compute_dist<LPE, NT>(P, S, PRE ? prw : nullptr);
     if (P.o.cforce && lane < N) {
       double fx, fy;
@@ -688,12 +611,18 @@ void rollout_team_kernel(const KParams* __restrict__ Pp, const KStep K) {
     }
     // the magnetic-field segment sums (partials in U2, read by the agent wave in D, before the
     // info rows reuse U2)
-    if (DYN == 0 && !P.use_filter_arg) magnetic_partials_wave<LPE, NT>(P, S, S.dpair);
+    if (mag) {
+      double* tab = S.dpair + 2 * LPE;
+      mag_table_store<LPE>(mr, tab);
+      esync<LPE>();
+      magnetic_partials_wave<LPE, NT>(P, S, S.dpair, tab);
+    }
     m_pre = chunked ? ego_mask(S, N, L, -1) : 0;
   }
   TSTAMP(7);
   __syncthreads();
   TSTAMP(3);
+  TSTOP(5);
 
   // ---- D. per-agent reward / info / stats (agent wave WD) while the other waves store their
   // env's adjacency speculatively (valid unless an agent changes done / reached status this step:
@@ -733,6 +662,7 @@ void rollout_team_kernel(const KParams* __restrict__ Pp, const KStep K) {
   TSTAMP(8);
   __syncthreads();
   TSTAMP(4);
+  TSTOP(6);
 
   // ---- E. info rows, dones, then what the speculation did not cover, or the auto-reset --------
   __shared__ int team_rs[G];   // this step's auto-resets of the workgroup's envs
@@ -770,7 +700,7 @@ void rollout_team_kernel(const KParams* __restrict__ Pp, const KStep K) {
     int p0 = 0;
     if (rs) p0 = team_reset_prep<DYN, NT>(P, S, env, K.cur_new);
     TSTAMP(19);
-    // each resetting env's wave draws its own scenario on all 64 lanes (random_scenario_wave):
+    // each resetting env's wave draws its own scenario on all 64 lanes (random_scenario_wave2):
     // reset steps 70.0-73.6 us vs 86.4-90.2 with round 3's one wave drawing lane g for env g
     // (profiles/r04_v1_reset_wdraw.json, r04_v2_reset_lanedraw.json, config 3)
     if (rs) team_scenario_wave<DYN, NT>(P, S, env, p0);

@@ -76,13 +76,27 @@ def _run_parallel(jobs, verbose=True):
         raise RuntimeError("compile failed: %s" % ", ".join(os.path.basename(f) for f in failed))
 
 
+def build_id(defines=()) -> str:
+    """sha256 of the step kernel's sources, the header, the compiler flags and the variant's -D
+    flags (16 hex digits): lsm_build_id() of the library built from them."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in _rollout_deps():
+        h.update(os.path.basename(f).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    h.update(" ".join(FLAGS + sorted(defines)).encode())
+    return h.hexdigest()[:16]
+
+
 def _rollout_jobs(defines=(), tag="", force=True, parts=None):
     jobs = []
+    bid = build_id(defines)
     for part in (range(ROLLOUT_PARTS) if parts is None else parts):
         o = _part_obj(part, tag)
         if force or _stale(o, _rollout_deps()):
-            cmd = [HIPCC] + FLAGS + ["-D%s" % d for d in defines] + ["-DLSM_PART=%d" % part, "-c", "-o", o + ".tmp",
-                                                                   "lsm_rollout.hip"]
+            cmd = [HIPCC] + FLAGS + ["-D%s" % d for d in defines] + ['-DLSM_BUILD_ID="%s"' % bid] + \
+                ["-DLSM_PART=%d" % part, "-c", "-o", o + ".tmp", "lsm_rollout.hip"]
             jobs.append((cmd, o))
     return jobs
 

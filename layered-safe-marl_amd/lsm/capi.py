@@ -37,7 +37,7 @@ EXPORTED = ("lsm_create", "lsm_destroy", "lsm_last_error", "lsm_set_value_table"
             "lsm_edges_last_error", "lsm_bind_output_ring", "lsm_select_ring", "lsm_buffer_insert",
             "lsm_buffer_last_error", "lsm_host_rk45_di", "lsm_host_glibc_pow", "lsm_action_errors",
             "lsm_kernel_name", "lsm_reset_layout", "lsm_layout_doubles", "lsm_host_philox_uniforms",
-            "lsm_host_philox4x32", "lsm_episode_summary")
+            "lsm_host_philox4x32", "lsm_episode_summary", "lsm_build_id", "lsm_test_set_mt_stage")
 
 
 class LsmConfig(C.Structure):
@@ -107,6 +107,8 @@ def load_library(path: str = LIB_PATH):
         "lsm_host_philox_uniforms": (I32, [U32, U32, I32, D, D, P]),
         "lsm_host_philox4x32": (I32, [P, P, P]),
         "lsm_episode_summary": (I32, [P, I32, P, P]),
+        "lsm_build_id": (C.c_char_p, []),
+        "lsm_test_set_mt_stage": (I32, [P, I32]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name, None)

@@ -8,6 +8,9 @@ counter(k) - counter(k-1) = what phase k issues.
     rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU -d D -o run \
         --output-format csv -- python3 -m lsm.diag_phasecount
     python -m lsm.diag_phasecount --reduce D
+
+``--team``: the team kernel's stops (lsm_team.h TSTOP): 1 record in LDS, 2 pair lookups, 3 end of
+phase A, 4 end of B, 5 end of C, 6 end of D, 7 the whole step (E).
 """
 from __future__ import annotations
 
@@ -17,11 +20,14 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 STOPS = list(range(0, 12))
+TEAM_STOPS = list(range(1, 8))
+TEAM_PHASES = ["A record", "A pairs", "A filter prep", "B agent wave", "C distances", "D reward/info",
+               "E outputs"]
 REPS = 4
 WARM = 6
 
 
-def run(config):
+def run(config, team=False):
     from .diag_stamps import STAMP_LIB
     os.environ["LSM_LIB"] = STAMP_LIB
     import torch
@@ -41,8 +47,8 @@ def run(config):
     gen = torch.Generator(device="cuda:0").manual_seed(0)
     for _ in range(WARM):   # full steps: a mid-episode state
         env.step(torch.randint(0, 25, (c["envs"], N), device="cuda:0", dtype=torch.int32, generator=gen), 4)
-    for k in STOPS:
-        os.environ["LSM_STOP_AFTER"] = str(k)
+    for k in (TEAM_STOPS if team else STOPS):
+        os.environ["LSM_STOP_AFTER"] = str(k if not (team and k == 7) else -1)
         for _ in range(REPS):
             env.step(torch.randint(0, 25, (c["envs"], N), device="cuda:0", dtype=torch.int32, generator=gen), 4)
     torch.cuda.synchronize()
@@ -50,12 +56,12 @@ def run(config):
     env.close()
 
 
-def reduce(d, config=3):
+def reduce(d, config=3, team=False):
     import statistics
     from .pmc import _rows
     per = {}
     for r in _rows(d, "counter_collection.csv"):
-        if "rollout_kernel" not in r.get("Kernel_Name", ""):
+        if ("lsm::rollout" if team else "rollout_kernel") not in r.get("Kernel_Name", ""):
             continue
         k = int(r.get("Dispatch_Id") or 0)
         per.setdefault(k, {})
@@ -63,21 +69,27 @@ def reduce(d, config=3):
     ids = sorted(per)
     # launches: reset (1) + WARM full steps + len(STOPS) * REPS
     ids = ids[1 + WARM:]
-    assert len(ids) == len(STOPS) * REPS, len(ids)
+    stops = TEAM_STOPS if team else STOPS
+    assert len(ids) == len(stops) * REPS, len(ids)
     names = sorted(per[ids[0]])
     waves = None
     cum = {}
-    for i, k in enumerate(STOPS):
+    for i, k in enumerate(stops):
         grp = ids[i * REPS:(i + 1) * REPS]
         cum[k] = {n: statistics.fmean(per[g][n] for g in grp) for n in names}
     from .diag_stamps import PHASES
     print("%-14s" % "phase" + "".join("%16s" % n for n in names) + "   (per wave)")
     prev = {n: 0.0 for n in names}
+    print("(per wave: counters / envs; the team kernel's agent-wave phases B and D run on one wave "
+          "of each 4, so their per-wave share is a quarter of that wave's)")
     sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
     import bench
     nw = float(bench.CONFIGS[config]["envs"])
-    for k in STOPS:
-        label = "start" if k == 0 else (PHASES[k - 1] if k <= len(PHASES) else "store")
+    for k in stops:
+        if team:
+            label = TEAM_PHASES[k - 1]
+        else:
+            label = "start" if k == 0 else (PHASES[k - 1] if k <= len(PHASES) else "store")
         print("%-14s" % label + "".join("%16.0f" % ((cum[k][n] - prev[n]) / nw) for n in names))
         prev = cum[k]
 
@@ -86,8 +98,9 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", type=int, default=3)
     ap.add_argument("--reduce", default=None)
+    ap.add_argument("--team", action="store_true")
     a = ap.parse_args()
     if a.reduce:
-        reduce(a.reduce, a.config)
+        reduce(a.reduce, a.config, a.team)
     else:
-        run(a.config)
+        run(a.config, a.team)

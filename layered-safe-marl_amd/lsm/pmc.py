@@ -8,7 +8,8 @@ one TCC pass on gfx950) and applies the gfx950 corrections of
 /opt/skills/guides/MI355X_MICROARCH.md (HBM section): FETCH_SIZE is in KiB and
 counts half the bytes of wide coalesced reads (x2), WRITE_SIZE is exact for
 16-B/lane streaming stores.  Values are per launch of ``rollout_kernel``
-(mean over the profiled dispatches, warm-up launches excluded).
+(mean over the profiled dispatches, warm-up launches excluded). Each entry records the
+``lsm_build_id()`` of the library that was profiled; bench.py quotes an entry only for that build.
 """
 from __future__ import annotations
 
@@ -78,6 +79,7 @@ def main():
     t.add_argument("--envs", type=int, required=True)
     t.add_argument("--out", default=None)
     t.add_argument("--kernel", default=KERNEL)
+    t.add_argument("--round", default=None, help="profile tag (e.g. r05) recorded with the entry")
     c = sub.add_parser("counters")
     c.add_argument("dirs", nargs="+")
     c.add_argument("--kernel", default=KERNEL)
@@ -104,7 +106,10 @@ def main():
         return
     fetch_kib, nf = counter_per_launch(a.fetch_dir, "FETCH_SIZE", a.kernel)
     write_kib, nw = counter_per_launch(a.write_dir, "WRITE_SIZE", a.kernel)
-    rec = {"num_envs": a.envs, "kernel": a.kernel, "fetch_size_kib_raw": fetch_kib, "write_size_kib": write_kib,
+    from . import capi
+    bid = capi.load_library().lsm_build_id().decode()
+    rec = {"num_envs": a.envs, "kernel": a.kernel, "build_id": bid, "round": a.round,
+           "fetch_size_kib_raw": fetch_kib, "write_size_kib": write_kib,
            "fetch_bytes_corrected": 2 * fetch_kib * 1024, "write_bytes": write_kib * 1024,
            "hbm_bytes_per_launch": 2 * fetch_kib * 1024 + write_kib * 1024,
            "dispatches": [nf, nw],

@@ -34,7 +34,7 @@ cd "$ROOT/layered-safe-marl_amd"
 python -m lsm.pmc stats "$OUT/ktrace" > "$ROOT/profiles/${ROUND}_config${CFG}_kernel_stats.txt"
 python -m lsm.pmc launches "$OUT/ktrace" --kernel "$KERN" > "$ROOT/profiles/${ROUND}_config${CFG}_launches.json"
 cp "$(find "$OUT/ktrace" -name '*kernel_stats.csv' | head -n1)" "$ROOT/profiles/${ROUND}_config${CFG}_kernel_stats.csv"
-python -m lsm.pmc traffic "$OUT/fetch" "$OUT/write" --config "$CFG" --envs "$ENVS" --kernel "$KERN" \
+python -m lsm.pmc traffic "$OUT/fetch" "$OUT/write" --config "$CFG" --envs "$ENVS" --kernel "$KERN" --round "$ROUND" \
     --out "$ROOT/profiles/pmc_traffic.json" > "$ROOT/profiles/${ROUND}_config${CFG}_traffic.json"
 python -m lsm.pmc counters "$OUT/sq1" "$OUT/sq2" --kernel "$KERN" > "$ROOT/profiles/${ROUND}_config${CFG}_sq_counters.txt"
 cp "$ROOT/profiles/"${ROUND}_config${CFG}_* "$ROOT/profiles/pmc_traffic.json" "$ROOT/gpurun_out/"

@@ -437,9 +437,19 @@ def main(only=None):
                          seed=56, ep=4, steps=130, ttr_stored=ttr_small, action_seed=26,
                          reward_terms=("potential_conflict", "safety_violation")),
     ]
+    # reward_reach_goal's bare `rew -= 1.0` (double integrator, filter on, not done, no goal reward)
+    # leaves a Python float, which the float32 HJ-value terms (stair ratio the int 1) keep float32
+    hjf = lambda: run_case("di_n8_rw_hjf", A(num_agents=8, num_env_steps=60 * 4, episode_length=60,
+                                             use_safety_filter=True, collaborative=True),
+                           seed=57, ep=4, steps=130, value_stored=di_small, action_seed=27,
+                           reward_terms=("hj_value",))
+    rewards.append(hjf)
     if only == "rewards":
         for f in rewards:
             f()
+        return
+    if only == "rw_hjf":
+        hjf()
         return
     if only == "sepcur":
         for f in sepcur:

@@ -61,6 +61,13 @@ def test_world_size_must_match_gpus():
     assert out.returncode != 0 and "WORLD_SIZE" in (out.stderr + out.stdout)
 
 
-def test_traffic_lookup_matches_workload():
-    assert bench.load_traffic(3, 4096) is None or bench.load_traffic(3, 4096) > 1e8
-    assert bench.load_traffic(3, 123) is None   # a different workload never borrows the number
+def test_traffic_lookup_matches_workload_and_build():
+    import json
+    import os
+    p = os.path.join(os.path.dirname(bench.__file__), "profiles", "pmc_traffic.json")
+    e = json.load(open(p)).get("config3", {})
+    bid = e.get("build_id")
+    if bid:
+        assert bench.load_traffic(3, e["num_envs"], bid) > 1e8
+    assert bench.load_traffic(3, 123, bid) is None       # a different workload never borrows the number
+    assert bench.load_traffic(3, 4096, "not-this-build") is None   # nor a different library build

@@ -132,6 +132,10 @@ CASES = [
     # ... and the HJ-value term with the filter off (the handle exists only for the reward)
     dict(dynamics_type="double_integrator", num_agents=5, world_size=4, episode_length=60,
          num_env_steps=60 * 4, use_safety_filter=False, ep=1, reward_terms=("hj_value", "safety_violation")),
+    # ... and the HJ-value term alone with the filter on: reward_reach_goal's Python-float base
+    # (`rew -= 1.0`) plus float32 terms stays float32 (fixture di_n8_rw_hjf)
+    dict(dynamics_type="double_integrator", num_agents=8, world_size=4, episode_length=60,
+         num_env_steps=60 * 4, use_safety_filter=True, ep=4, collaborative=True, reward_terms=("hj_value",)),
 ]
 
 
@@ -689,13 +693,14 @@ def test_gpu_team_kernel_resets_match_oracle(dyn, N, team, monkeypatch):
     resetting env's wave draws its scenario with the agents in parallel from the staged MT19937
     stream, crossing block boundaries over successive resets) against the oracle: 10-step episodes,
     75 steps (7 resets per env), envs driven all-done early at different steps so resets do not line
-    up, every output. "4s": the staged stream serves only 40 words (LSM_MT_STAGE), so every draw runs
+    up, every output. "4s": the staged stream serves only 40 words (lsm_test_set_mt_stage), so every draw runs
     out and takes the cooperative redraw, whose stream state goes back to HBM."""
     import torch
     if dyn == "airtaxi" and team == "8":
         pytest.skip("8 airtaxi envs of 16 agents do not fit one 64-lane agent wave")
+    stage = None
     if team == "4s":
-        monkeypatch.setenv("LSM_MT_STAGE", "40")
+        stage = 40
         team = "4"
     monkeypatch.setenv("LSM_TEAM", team)
     ws = 4 if dyn == "double_integrator" else 6
@@ -704,6 +709,8 @@ def test_gpu_team_kernel_resets_match_oracle(dyn, N, team, monkeypatch):
                 num_internal_step=1, seed=21, env_seed=21)
     n_envs = 15   # a partly filled last workgroup
     env = _gpu_env(meta, n_envs=n_envs, seed=21)
+    if stage is not None:
+        assert env.lib.lsm_test_set_mt_stage(env.h, stage) == 0
     assert env.kernel_name.startswith("rollout_team_kernel<")
     ora = _oracle_for(meta, 21, n_envs)
     g, o = env.reset(4), ora.reset(4)
