@@ -785,26 +785,6 @@ __device__ __forceinline__ void interp_grad(const TableDev& T, const double* s, 
   }
 }
 
-// interp_grad with the 2^ND corner gradients of the query's cell already in LDS (lc, gw = 1:
-// the team kernel's speculative prefetch), same weights and summation order
-template <int ND>
-__device__ __forceinline__ void interp_grad_lds(const TableDev& T, const double* s, const f32x4* lc, float* g) {
-  int cell;
-  float w[1 << ND];
-  for (int d = 0; d < ND; ++d) g[d] = 0.0f;
-  if (!grid_cell<ND>(T, s, cell, w)) {
-    for (int d = 0; d < ND; ++d) g[d] = __builtin_nanf("");
-    return;
-  }
-#pragma unroll
-  for (int c = 0; c < (1 << ND); ++c) {
-    const f32x4 a = lc[c];
-    const float gv[4] = {a.x, a.y, a.z, a.w};
-#pragma unroll
-    for (int d = 0; d < ND; ++d) g[d] = g[d] + w[c] * gv[d];
-  }
-}
-
 // Bounds of the interpolated value at s: the (widened) min / max of the block containing
 // its cell. Same in-range decision and cell index as grid_cell(); false = out of the grid
 // (the lookup is +inf, no load).
@@ -1102,7 +1082,6 @@ __device__ __forceinline__ double magnetic_penalty_agent(const KParams& P, const
     blas_rot(c, s, S.ps[i] - gxx, S.ps[N + i] - gyy, qx, qy);
     const double dist = blas_norm2(qx, qy);
     blas_rot(c, s, S.ps[2 * N + i] - 0.0, S.ps[3 * N + i] - 0.0, rvx, rvy);
-#ifdef LSM_AB_MAGID
     // cos / sin of atan2(y, x) as x / |(x, y)|, y / |(x, y)| (ulp-level vs the reference's
     // np.cos(np.arctan2(..)), inside the reward tolerance); the origin keeps atan2's signed zeros
     double ch = 1.0, sh = 0.0;
@@ -1129,25 +1108,6 @@ __device__ __forceinline__ double magnetic_penalty_agent(const KParams& P, const
     const double rfx = ref_speed * ch, rfy = ref_speed * sh;
     const double err = blas_norm2(rvx - rfx, rvy - rfy);
     const double cp = (dist > 0.0 && dist < INFINITY) ? qx / dist : cos(atan2(qy, qx));
-#else
-    const double polar = atan2(qy, qx);
-    double href = 0.0;
-    if (!(fabs(qx) < 1e-6)) {
-      double s0 = 0.0, s1 = 0.0;
-      for (int q = 0; q < G; ++q) {
-        s0 += part[i * G + q];
-        s1 += part[LPE + i * G + q];
-      }
-      s0 = s0 / 0.5;
-      href = atan2(s1, s0);
-    }
-    double ref_speed = py_max(gs, 0.1);
-    const double dr = np_clip(dist / 1.5, 0, 1);
-    ref_speed = ref_speed * (1 - dr) + 1.0 * dr;
-    const double rfx = ref_speed * cos(href), rfy = ref_speed * sin(href);
-    const double err = blas_norm2(rvx - rfx, rvy - rfy);
-    const double cp = cos(polar);
-#endif
     if (cp < P.cos_pi6) {
       pen = err;
     } else {
@@ -1293,11 +1253,8 @@ __device__ __forceinline__ void filter_qp(const KParams& P, const Lds& S, int i,
                                           const double* rel, const float* g, uint8_t& filtered, double& u0,
                                           double& u1);
 
-// gpc / gpj (team kernel, double integrator): the gradient corners prefetched for ego i's partner
-// gpj[i] (the previous step's deconflicting agent), used when the argmin picks that partner
 template <int DYN, int NT>
-__device__ __forceinline__ void filter_prep(const KParams& P, Lds& S, int i, const f32x4* gpc = nullptr,
-                                            const int* gpj = nullptr) {
+__device__ __forceinline__ void filter_prep(const KParams& P, Lds& S, int i) {
   LSM_DIMS;
   float* f = filter_slot(S, N, i);
   int st = 0, jv = -1;
@@ -1313,9 +1270,7 @@ __device__ __forceinline__ void filter_prep(const KParams& P, Lds& S, int i, con
       st = 3;
       double rel[5];
       rel_state<DYN>(S, N, i, jv, rel);
-      if (DYN == 0 && gpj && gpj[i] == jv) interp_grad_lds<4>(P.val, rel, gpc + 16 * i, g);
-      else if (DYN == 0) interp_grad<4>(P.val, rel, g);
-      else interp_grad<5>(P.val, rel, g);
+      if (DYN == 0) interp_grad<4>(P.val, rel, g); else interp_grad<5>(P.val, rel, g);
     }
   }
   float4* f4 = (float4*)f;
@@ -2427,8 +2382,19 @@ __device__ __forceinline__ double rk_norm4_pair(double mp, double mv, bool up) {
 
 // rk45_di for one axis (position p, velocity v, acceleration a) of a lane pair; `up` = y axis.
 // Both lanes of a pair reach the same scalar decisions (same norms), so they stay in step.
-__device__ __forceinline__ void rk45_di_pair(double& p, double& v, double a, double tb, bool up) {
+__device__ __forceinline__ void rk45_di_pair(double& p, double& v, double a, double tb, bool up,
+                                             PowTabs pt = PowTabs()) {
   const double rtol = 1e-3, atol = 1e-6;
+  // At rest with no acceleration on both axes (+0.0 velocity and acceleration, position not -0.0)
+  // every stage is +-0 and every step leaves (p, v) as they are: the result without the ~6 steps
+  // that select_initial_step's 1e-6 start takes to reach tb (its values feed nothing else).
+  {
+    const bool rest = __double_as_longlong(v) == 0 && __double_as_longlong(a) == 0 &&
+                      __double_as_longlong(p) != (long long)0x8000000000000000ull;
+    const bool prest = lane32_partner(rest ? 1.0 : 0.0) != 0.0;
+    if (rest && prest) return;
+  }
+
   const Rk45Tab& T = rk45_tab();
   double dv[6];
 #pragma unroll
@@ -2444,7 +2410,7 @@ __device__ __forceinline__ void rk45_di_pair(double& p, double& v, double a, dou
   if (d1 <= 1e-15 && d2 <= 1e-15) {
     h1 = (h0 * 1e-3 > 1e-6) ? h0 * 1e-3 : 1e-6;
   } else {
-    h1 = glibc_pow(0.01 / ((d2 > d1) ? d2 : d1), 1.0 / 5.0);
+    h1 = glibc_pow(0.01 / ((d2 > d1) ? d2 : d1), 1.0 / 5.0, pt);
   }
   double h_abs = 100 * h0;
   if (h1 < h_abs) h_abs = h1;
@@ -2466,15 +2432,24 @@ __device__ __forceinline__ void rk45_di_pair(double& p, double& v, double a, dou
       const double ynv = v + h * gb;
       k[6] = ynv;
       const double ep = rk_gemv_col(k, T.E, 7), ev = ge;
-      const double ap = fabs(p), anp = fabs(ynp), av = fabs(v), anv = fabs(ynv);
-      const double rp = (ep * h) / (atol + ((ap >= anp) ? ap : anp) * rtol);
-      const double rv = (ev * h) / (atol + ((av >= anv) ? av : anv) * rtol);
-      const double en = rk_norm4_pair(rp, rv, up);
+      // The error terms are rounding noise for this ODE (the stages are exact up to rounding):
+      // when |e h| <= 1e-13 on all four components, each scaled term is <= 1e-7 (denominators
+      // >= atol = 1e-6), so the computed norm is < 1e-6: the step is accepted with factor 10
+      // (no pow), exactly the branch the full computation takes. Otherwise the full computation.
+      const bool mine = fabs(ep * h) <= 1e-13 && fabs(ev * h) <= 1e-13;   // NaN: not small
+      const bool small = mine && lane32_partner(mine ? 1.0 : 0.0) != 0.0;
+      double en = 0.0;
+      if (!small) {
+        const double ap = fabs(p), anp = fabs(ynp), av = fabs(v), anv = fabs(ynv);
+        const double rp = (ep * h) / (atol + ((ap >= anp) ? ap : anp) * rtol);
+        const double rv = (ev * h) / (atol + ((av >= anv) ? av : anv) * rtol);
+        en = rk_norm4_pair(rp, rv, up);
+      }
       if (en < 1) {
         if (t_new < tb) {
           double fac = 10.0;
           if (en > 1e-6) {
-            const double q = 0.9 * glibc_pow(en, -1.0 / 5.0);
+            const double q = 0.9 * glibc_pow(en, -1.0 / 5.0, pt);
             if (q < fac) fac = q;
           }
           if (rejected && fac > 1) fac = 1;
@@ -2486,7 +2461,7 @@ __device__ __forceinline__ void rk45_di_pair(double& p, double& v, double a, dou
         v0 = ynv;
         break;
       }
-      const double q = 0.9 * glibc_pow(en, -1.0 / 5.0);
+      const double q = 0.9 * glibc_pow(en, -1.0 / 5.0, pt);
       h_abs *= (q > 0.2) ? q : 0.2;
       rejected = true;
     }
@@ -2494,11 +2469,12 @@ __device__ __forceinline__ void rk45_di_pair(double& p, double& v, double a, dou
 }
 
 // integrate_agent<0> on a lane pair (axis `up` of agent i): RK45, speed clamp, travel distance
-__device__ __forceinline__ void integrate_agent_di_pair(const KParams& P, Lds& S, int N, int i, bool up) {
+__device__ __forceinline__ void integrate_agent_di_pair(const KParams& P, Lds& S, int N, int i, bool up,
+                                                        PowTabs pt = PowTabs()) {
   const int c = up ? 1 : 0;
   double p = S.ps[c * N + i], v = S.ps[(2 + c) * N + i];
   const double a = S.safe[c * N + i];
-  rk45_di_pair(p, v, a, P.dt, up);
+  rk45_di_pair(p, v, a, P.dt, up, pt);
   double q = lane32_partner(v);
   double sx = up ? q : v, sy = up ? v : q;
   double spd = sqrt(sx * sx + sy * sy);
@@ -3026,13 +3002,8 @@ __device__ __forceinline__ void decode_action(const KParams& P, Lds& S, int N, i
   if (ai < 0 || ai > 24) *gptr(P.action_err) = 1;
   const int a = ai < 0 ? 0 : (ai > 24 ? 24 : ai);
   const int xi = a / 5, yi = a - xi * 5;
-#ifdef LSM_AB_DEC
   S.raw[i] = sel5(P.act0, xi);
   S.raw[N + i] = sel5(P.act1, yi);
-#else
-  S.raw[i] = P.act0[xi];
-  S.raw[N + i] = P.act1[yi];
-#endif
 }
 
 // Safety filter of agent i once the pair scratch is filled (core.py:648-677): the filtered

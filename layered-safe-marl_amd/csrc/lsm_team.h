@@ -432,6 +432,20 @@ void rollout_team_kernel(const KParams* __restrict__ Pp, const KStep K) {
   int act = 0;
   int cstep = 0;
   bool filter_on = false;
+  // the agent wave's pow tables (lsm_rk45.h PowTabs) for its lane-pair RK45: 192 float4 of log rows
+  // into env 0's U1 and 128 float4 of exp pairs into env 1's U1 (both free until the distances), a
+  // slice per wave, issued with the record. The table loads inside pow were L2 round trips on the
+  // latency-bound phase B: 32.40 -> 31.75 us per step at config 3 (profiles/r05_v3_ab_c3_powlds.txt)
+  constexpr int NPQ = (320 + 64 * G - 1) / (64 * G);
+  f32x4 ptq[NPQ];
+  if (DYN == 0 && G * NT <= 32 && K.mode == 0) {
+#pragma unroll
+    for (int r = 0; r < NPQ; ++r) {
+      const int q = lane + 64 * (w + G * r);
+      const GAS f32x4* src = q < 192 ? (const GAS f32x4*)powl_tab(0) + q : (const GAS f32x4*)expd_tab_ptr() + (q - 192);
+      ptq[r] = *(q < 320 ? src : (const GAS f32x4*)powl_tab(0));
+    }
+  }
   if (live) {
     if (K.mode == 0 && lane < N) act = read_action(K, env, N, lane);
     if (PRE) {
@@ -488,31 +502,6 @@ void rollout_team_kernel(const KParams* __restrict__ Pp, const KStep K) {
     if (lane < N) decode_action(P, S, N, lane, act);
     filter_on = S.cur[C_FILT] != 0.0;
     if (filter_on) {
-#ifdef LSM_AB_GPRE
-      // The gradient lookup of each ego at its previous step's deconflicting agent (record decon),
-      // issued with the pair lookups: the argmin picks the same agent in ~99 % of filtered egos, and
-      // then its gradient needs no second memory round trip after the argmin (filter_prep). Lane l
-      // loads corner l % 16 of ego l / 16 (+ 4); parked in U1 (free until the distances).
-      f32x4 gq[2];
-      int gpj[2];
-      if (DYN == 0 && NT == 8) {
-#pragma unroll
-        for (int r = 0; r < 2; ++r) {
-          const int e = (lane >> 4) + 4 * r, c = lane & 15;
-          int pj = S.decon[e];
-          bool ok = pj >= 0 && pj < N && pj != e && !inactive_pre(S, e) && !inactive_pre(S, pj);
-          int cell = 0;
-          if (ok) {
-            double rel[5];
-            float w[16];
-            rel_state<DYN>(S, N, e, pj, rel);
-            ok = grid_cell<4>(P.val, rel, cell, w);
-          }
-          gpj[r] = ok ? pj : -1;
-          gq[r] = ((const GAS f32x4*)gptr(P.val.gcells))[ok ? (size_t)cell * 16 + c : (size_t)c];
-        }
-      }
-#endif
       const SepChain sc = sep_chain(S.sep, P.s, env);
       for (int p = lane; p < N * N; p += LPE) {
         const int j = p / N, i = p - j * N;   // [j][i]: ego i fastest (bank-conflict-free reads)
@@ -531,24 +520,17 @@ void rollout_team_kernel(const KParams* __restrict__ Pp, const KStep K) {
       TSTOP(2);
       // the deconflicting choice and the HJ gradient lookup of every ego, here where the other
       // waves of the SIMD hide the gather; the agent wave does the QP in B (filter_agent_slot)
-#ifdef LSM_AB_GPRE
-      f32x4* gpc = (f32x4*)S.fval;
-      int* gpi = (int*)(gpc + 16 * NT);
-      if (DYN == 0 && NT == 8) {
-#pragma unroll
-        for (int r = 0; r < 2; ++r) {
-          const int e = (lane >> 4) + 4 * r;
-          gpc[16 * e + (lane & 15)] = gq[r];
-          if ((lane & 15) == 0) gpi[e] = gpj[r];
-        }
-      }
-      esync<LPE>();
-      if (lane < N) filter_prep<DYN, NT>(P, S, lane, gpc, (DYN == 0 && NT == 8) ? gpi : nullptr);
-#else
       esync<LPE>();
       if (lane < N) filter_prep<DYN, NT>(P, S, lane);
-#endif
       TSTAMP(17);
+    }
+  }
+  if (DYN == 0 && G * NT <= 32 && K.mode == 0) {
+#pragma unroll
+    for (int r = 0; r < NPQ; ++r) {
+      const int q = lane + 64 * (w + G * r);
+      if (q < 192) ((f32x4*)carve(smem, N, NL, E, F, false).fval)[q] = ptq[r];
+      else if (q < 320) ((f32x4*)carve(smem + B, N, NL, E, F, false).fval)[q - 192] = ptq[r];
     }
   }
   TSTAMP(6);
@@ -580,7 +562,10 @@ void rollout_team_kernel(const KParams* __restrict__ Pp, const KStep K) {
       const int g2 = hl / NT, i2 = hl - g2 * NT;
       if (g2 < G && env0 + g2 < P.n_envs) {
         Lds A2 = carve(smem + (size_t)g2 * B, N, NL, E, F, false);
-        if (!A2.dpre[i2]) integrate_agent_di_pair(P, A2, N, i2, lane >= 32);
+        PowTabs pt;
+        pt.log = (const double*)carve(smem, N, NL, E, F, false).fval;
+        pt.exp = (const uint64_t*)carve(smem + B, N, NL, E, F, false).fval;
+        if (!A2.dpre[i2]) integrate_agent_di_pair(P, A2, N, i2, lane >= 32, pt);
       }
     } else if (alane && !A.dpre[ai]) {
       integrate_agent<DYN>(P, A, N, ai);

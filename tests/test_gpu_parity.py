@@ -221,6 +221,7 @@ def test_gpu_matches_oracle_multi_env(case, lpe, monkeypatch):
     np.testing.assert_allclose(g[2], o[1][:n], rtol=0, atol=F32_ATOL)
     np.testing.assert_array_equal(g[3] != 0, o[2][:n] != 0)
     mism = 0
+    drew = dind = 0.0
     for t, r in enumerate(run["steps"]):
         g = env.step(r["a"][:n], ep)
         ctx = "case %d step %d" % (case, t)
@@ -230,14 +231,19 @@ def test_gpu_matches_oracle_multi_env(case, lpe, monkeypatch):
         np.testing.assert_allclose(g[2], r["node"][:n], rtol=0, atol=F32_ATOL, err_msg=ctx)
         np.testing.assert_allclose(g[3], r["adj"][:n], rtol=0, atol=F32_ATOL, err_msg=ctx)
         np.testing.assert_allclose(g[4], r["rew"][:n], rtol=1e-6, atol=1e-5, err_msg=ctx)
-        np.testing.assert_allclose(env.t_info.cpu().numpy()[:, :, _info_col("individual_reward")],
-                                   r["ind_rew"][:n], rtol=1e-9, atol=1e-9, err_msg=ctx + " individual_reward")
+        ind = env.t_info.cpu().numpy()[:, :, _info_col("individual_reward")]
+        np.testing.assert_allclose(ind, r["ind_rew"][:n], rtol=1e-9, atol=1e-9, err_msg=ctx + " individual_reward")
+        drew = max(drew, float(np.abs(np.asarray(g[4], dtype=np.float64).reshape(n, -1) -
+                                      np.asarray(r["rew"][:n], dtype=np.float64).reshape(n, -1)).max()))
+        dind = max(dind, float(np.abs(ind - r["ind_rew"][:n]).max()))
         st = env.state().cpu().numpy()
         np.testing.assert_allclose(st, r["state"][:n], rtol=0, atol=STATE_ATOL, err_msg=ctx)
         mism += int(np.any(st != r["state"][:n], axis=(1, 2)).sum())
     # states are compared at STATE_ATOL; how many env-steps were not bit-identical is reported
     print("state_mismatch case=%d lpe=%s env_steps_not_bit_identical=%d of %d" % (case, lpe, mism,
                                                                               len(run["steps"]) * n))
+    # the largest reward deviations from the oracle (float32 output; float64 individual_reward)
+    print("reward_deviation case=%d lpe=%s max_abs_reward=%.3g max_abs_individual_reward=%.3g" % (case, lpe, drew, dind))
     env.close()
 
 

@@ -47,6 +47,12 @@ def _cases(n, seed):
         if kind == 2 and rng.random() < 0.3:
             p = np.zeros(2)
         out.append((np.array([p[0], p[1], v[0], v[1]]), np.asarray(a, dtype=np.float64)))
+    # at rest with no acceleration (the kernels skip the integration there), signed zeros included
+    for p0 in (0.0, -0.0, 1.5):
+        for v0 in (0.0, -0.0):
+            for a0 in (0.0, -0.0):
+                out.append((np.array([p0, -2.25, v0, 0.0]), np.array([a0, 0.0])))
+                out.append((np.array([p0, 0.0, 0.0, v0]), np.array([0.0, a0])))
     return out
 
 
