@@ -357,6 +357,12 @@ def main():
     # Kernel time: HIP events on the launch stream bracketing the whole timed region (per-launch
     # event pairs would add their own GPU-side markers between back-to-back launches).
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    # no Python garbage collection inside the window: a collection pass stalls the host for ~0.1 ms,
+    # and with the launch queue that shallow the GPU idles (a 73 us gap in
+    # profiles/r05_v3_driver_window.txt)
+    import gc
+    gc.collect()
+    gc.disable()
     torch.cuda.synchronize()
     barrier(a.dist_backend)
     torch.cuda.synchronize()
@@ -369,6 +375,7 @@ def main():
     barrier(a.dist_backend)
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    gc.enable()
     kern_ms = ev0.elapsed_time(ev1) / a.steps   # includes the inter-launch gaps (conservative)
     per_rank = [elapsed * 1e3 / a.steps]
     if world > 1:

@@ -2382,8 +2382,18 @@ __device__ __forceinline__ double rk_norm4_pair(double mp, double mv, bool up) {
 
 // rk45_di for one axis (position p, velocity v, acceleration a) of a lane pair; `up` = y axis.
 // Both lanes of a pair reach the same scalar decisions (same norms), so they stay in step.
+#ifdef LSM_STAMPS
+// diagnostic build: s_memtime of lane 0 inside the agent wave's integration (lsm.diag_stamps --team)
+#define PSTAMP(k)                                                                                  \
+  do {                                                                                             \
+    if (stp && (threadIdx.x & 63) == 0) stp[k] = __builtin_amdgcn_s_memtime();                     \
+  } while (0)
+#else
+#define PSTAMP(k) do { } while (0)
+#endif
 __device__ __forceinline__ void rk45_di_pair(double& p, double& v, double a, double tb, bool up,
-                                             PowTabs pt = PowTabs()) {
+                                             PowTabs pt = PowTabs(), GAS unsigned long long* stp = nullptr) {
+  (void)stp;
   const double rtol = 1e-3, atol = 1e-6;
   // At rest with no acceleration on both axes (+0.0 velocity and acceleration, position not -0.0)
   // every stage is +-0 and every step leaves (p, v) as they are: the result without the ~6 steps
@@ -2417,6 +2427,7 @@ __device__ __forceinline__ void rk45_di_pair(double& p, double& v, double a, dou
   if (tb < h_abs) h_abs = tb;
   double t = 0.0;
   double v0 = v;   // K[0] of the step: the step's starting velocity
+  PSTAMP(27);
   while (t < tb) {
     bool rejected = false;
     for (;;) {
@@ -2470,11 +2481,14 @@ __device__ __forceinline__ void rk45_di_pair(double& p, double& v, double a, dou
 
 // integrate_agent<0> on a lane pair (axis `up` of agent i): RK45, speed clamp, travel distance
 __device__ __forceinline__ void integrate_agent_di_pair(const KParams& P, Lds& S, int N, int i, bool up,
-                                                        PowTabs pt = PowTabs()) {
+                                                        PowTabs pt = PowTabs(),
+                                                        GAS unsigned long long* stp = nullptr) {
   const int c = up ? 1 : 0;
   double p = S.ps[c * N + i], v = S.ps[(2 + c) * N + i];
   const double a = S.safe[c * N + i];
-  rk45_di_pair(p, v, a, P.dt, up, pt);
+  PSTAMP(29);
+  rk45_di_pair(p, v, a, P.dt, up, pt, stp);
+  PSTAMP(28);
   double q = lane32_partner(v);
   double sx = up ? q : v, sy = up ? v : q;
   double spd = sqrt(sx * sx + sy * sy);

@@ -565,7 +565,12 @@ void rollout_team_kernel(const KParams* __restrict__ Pp, const KStep K) {
         PowTabs pt;
         pt.log = (const double*)carve(smem, N, NL, E, F, false).fval;
         pt.exp = (const uint64_t*)carve(smem + B, N, NL, E, F, false).fval;
-        if (!A2.dpre[i2]) integrate_agent_di_pair(P, A2, N, i2, lane >= 32, pt);
+#ifdef LSM_STAMPS
+        GAS unsigned long long* stp = gptr(P.stamps) ? gptr(P.stamps) + (size_t)env * LSM_NSTAMP : nullptr;
+#else
+        GAS unsigned long long* stp = nullptr;
+#endif
+        if (!A2.dpre[i2]) integrate_agent_di_pair(P, A2, N, i2, lane >= 32, pt, stp);
       }
     } else if (alane && !A.dpre[ai]) {
       integrate_agent<DYN>(P, A, N, ai);

@@ -99,7 +99,8 @@ def main():
         ag = np.concatenate(tstamps12, axis=0)
         for name, i, j in [("A record", 0, 12), ("A decode+pairs", 12, 16), ("A argmin+grad", 16, 17),
                            ("A decode..prep", 12, 6), ("B filter", 1, 9),
-                           ("B integrate", 9, 2), ("D reward", 3, 10),
+                           ("B integrate", 9, 2), ("B: to RK45 start", 9, 29), ("B: initial step", 29, 27),
+                           ("B: RK45 steps", 27, 28), ("B: clamp+sync", 28, 2), ("D reward", 3, 10),
                            ("D info", 10, 11), ("D rows+stats", 11, 8), ("E info/dones", 4, 18),
                            ("E graph+record", 18, 5), ("R prep", 18, 19), ("R prep->draws", 19, 20),
                            ("R finish+dist", 20, 21), ("R emit", 21, 22), ("R store", 22, 5),
