@@ -398,7 +398,8 @@ def main():
     sb = step_bytes(N, 2, c["dynamics_type"], c["use_safety_filter"], layout)
     bytes_launch = sb["hbm_bytes"] * n_envs
     achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
-    build_id = env.lib.lsm_build_id().decode()
+    # (an A/B run may load an older library without lsm_build_id: tools/ab_bench.py --allow-old)
+    build_id = env.lib.lsm_build_id().decode() if hasattr(env.lib, "lsm_build_id") else "unknown"
     traffic = load_traffic(a.config, n_envs, build_id)
     resets = int((pre + a.steps) // epl - pre // epl)
     if rank == 0:

@@ -24,6 +24,7 @@
 // dense contraction; the kernel is bound by HBM writes of the dense per-ego outputs.
 #include <hip/hip_runtime.h>
 #include <math.h>
+#include <cmath>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -114,6 +115,10 @@ struct TableDev {
   int cstride[5];  // cell strides (cells per dim: n (periodic) or n - 1)
   float lo[5];
   float sp[5];
+  float rsp[5];    // 1 / sp (float32, correctly rounded)
+  int mdiv[5];     // 1: (s - lo) / sp by the reciprocal + one FMA correction (grid_pos), checked at
+                   // upload to equal the division bit for bit over every float32 the lookups can
+                   // meet (mdiv_check_kernel); 0: the division
   int periodic[5];
   int gw;  // float4 per corner gradient (1 for <= 4 dims, 2 for 5 dims)
   // Value bounds per block of 2^bshift cells per dim: (min, max) of the block's nodes widened
@@ -184,7 +189,8 @@ struct KParams {
   int64_t seed, env_offset;   // Philox keys: seed + 1000 * (env_offset + env)
   uint32_t lds_dep_off;       // LSM_SCENARIO_DEPARTURES: LDS offset of the departure arrays
   double dt, world_size, coord_range, world_eng, sep_target, max_speed, min_speed, gs_min, gs_max;
-  double coord_range2;   // coord_range^2 (float64-rounded)
+  double coord_range_s;  // the largest double s with sqrt(s) <= coord_range (correctly rounded sqrt):
+                         // sqrt(s) > coord_range <=> s > coord_range_s, for squared distances s >= 0
   double act0[5], act1[5];
   double mag_c[50], mag_s[50];
   double cos_pi6, two_pi, pi;
@@ -658,13 +664,24 @@ struct WaveRng {
 // Every dimension is computed without an early exit and the decision taken once at the end:
 // the table's per-dimension constants then load together instead of one scalar round trip per
 // dimension behind each exit (the latency-bound agent wave runs this in the filter).
+// The grid coordinate y / sp (y = s - lo in float32): the IEEE division, or -- where the upload check
+// found them equal for every float32 y the lookups can meet -- q = y r, q + (y - q sp) r with
+// r = 1 / sp (Markstein's correction, two FMAs instead of the ~10-instruction division sequence).
+__host__ __device__ __forceinline__ float grid_pos(float y, float sp, float rsp, int mdiv) {
+  if (!mdiv) return y / sp;
+  const float q = y * rsp;
+  const float r = fmaf(-q, sp, y);
+  return fmaf(r, rsp, q);
+}
+
 template <int ND>
 __device__ __forceinline__ bool grid_cell(const TableDev& T, const double* s, int& cell, float* w) {
-  float lo[ND], sp[ND];
-  int nn[ND], per[ND], cs[ND];
+  float lo[ND], sp[ND], rs[ND];
+  int nn[ND], per[ND], cs[ND], md[ND];
 #pragma unroll
   for (int d = 0; d < ND; ++d) {
     lo[d] = T.lo[d]; sp[d] = T.sp[d]; nn[d] = T.n[d]; per[d] = T.periodic[d]; cs[d] = T.cstride[d];
+    rs[d] = T.rsp[d]; md[d] = T.mdiv[d];
   }
   float wl[ND], wh[ND];
   int il[ND];
@@ -672,7 +689,7 @@ __device__ __forceinline__ bool grid_cell(const TableDev& T, const double* s, in
 #pragma unroll
   for (int d = 0; d < ND; ++d) {
     const float sd = (float)s[d];
-    float p = (sd - lo[d]) / sp[d];
+    float p = grid_pos(sd - lo[d], sp[d], rs[d], md[d]);
     ok = ok && (p == p) && !(fabsf(p) > 1.0e9f);   // NaN / runaway coordinate: outside
     if (!ok) p = 0.0f;                              // keeps the index math finite (result unused)
     const int n = nn[d];
@@ -795,7 +812,7 @@ __device__ __forceinline__ bool value_bounds(const TableDev& T, const double* s,
 #pragma unroll
   for (int d = 0; d < ND; ++d) {
     float sd = (float)s[d];
-    float p = (sd - T.lo[d]) / T.sp[d];
+    float p = grid_pos(sd - T.lo[d], T.sp[d], T.rsp[d], T.mdiv[d]);
     if (!(p == p) || fabsf(p) > 1.0e9f) return false;
     const int n = T.n[d];
     int f = (int)floorf(p);
@@ -859,6 +876,20 @@ __global__ void bounds_kernel(const float* values, float2* bnd, TableDev T, int 
   }
   const float m = 4.0e-6f * fmaxf(fabsf(mn), fabsf(mx));
   bnd[b] = make_float2(mn - m, mx + m);
+}
+#endif
+
+#if LSM_HOST_PART
+// grid_pos's reciprocal path against the division for every float32 y in [-neg, pos] (bit patterns
+// 0 .. pos_bits and the sign-flipped 0 .. neg_bits): bad = 1 on any difference (NaN == NaN).
+__global__ void mdiv_check_kernel(float sp, float rsp, uint32_t pos_bits, uint32_t neg_bits, int* bad) {
+  const uint64_t n = (uint64_t)pos_bits + 1 + (uint64_t)neg_bits + 1;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t b = i <= pos_bits ? (uint32_t)i : 0x80000000u | (uint32_t)(i - pos_bits - 1);
+    const float y = __uint_as_float(b);
+    const float a = grid_pos(y, sp, rsp, 0), c = grid_pos(y, sp, rsp, 1);
+    if (__float_as_uint(a) != __float_as_uint(c) && !(a != a && c != c)) *bad = 1;
+  }
 }
 #endif
 
@@ -1276,6 +1307,67 @@ __device__ __forceinline__ void filter_prep(const KParams& P, Lds& S, int i) {
   float4* f4 = (float4*)f;
   f4[0] = make_float4(g[0], g[1], g[2], g[3]);
   f4[1] = make_float4(g[4], vmin, __int_as_float(jv), __int_as_float(st));
+}
+
+// filter_prep of the double integrator's team kernel at N = 8 on all 64 lanes: lane 8 e + k is
+// ego e's candidate k. The argmins are butterflies over the 8 lanes of an ego (the lower index wins
+// ties, np.argmin's first occurrence, as filter_select); the gradient lookup of an applying ego runs
+// one component per lane (lanes k < 4, 16 corner loads of 4 B each) with interp_grad's weights and
+// summation order; lanes k write word k of the ego's slot. Same slots as filter_prep on 8 lanes,
+// about a third fewer vector instructions for the wave.
+template <int NT>
+__device__ __forceinline__ void filter_prep_oct(const KParams& P, Lds& S) {
+  constexpr int DYN = 0;
+  static_assert(NT == 8, "8 egos x 8 candidate lanes");
+  LSM_DIMS;
+  const int lane = threadIdx.x & 63;
+  const int e = lane >> 3, k = lane & 7;
+  const bool eact = !inactive_pre(S, e);
+  const bool kact = k != e && !inactive_pre(S, k);
+  // candidate k of ego e ([other][ego] pair matrices; the team kernel's pair loop stores squared
+  // distances: the nearest agent's only use is the coordination-range test, sqrt is monotone)
+  double d = S.dpair[k * N + e];
+  float v = (float)S.vpair[k * N + e];
+  bool in = S.inr[k * N + e] != 0;
+  int jd = kact ? k : 64, jv = kact ? k : 64;   // 64: no candidate
+#pragma unroll
+  for (int m = 1; m < 8; m <<= 1) {
+    const double od = __shfl_xor(d, m);
+    const float ov = __shfl_xor(v, m);
+    const int ojd = __shfl_xor(jd, m), ojv = __shfl_xor(jv, m);
+    const bool oin = __shfl_xor((int)in, m) != 0;
+    // take the other lane's candidate if it exists and is smaller, or equal with a lower index
+    const bool td = ojd < 64 && (jd == 64 || od < d || (od == d && ojd < jd));
+    const bool tv = ojv < 64 && (jv == 64 || ov < v || (ov == v && ojv < jv));
+    d = td ? od : d;
+    jd = td ? ojd : jd;
+    v = tv ? ov : v;
+    jv = tv ? ojv : jv;
+    in = tv ? oin : in;
+  }
+  int st = 0;
+  if (eact) st = jd == 64 ? 1 : ((!(d > P.coord_range_s) && in) ? 3 : 2);
+  if (st < 2) jv = -1;
+  const float vmin = st >= 2 ? v : 0.0f;
+  float gk = 0.0f;   // gradient component k (k < 4)
+  if (st == 3) {
+    double rel[5];
+    rel_state<DYN>(S, N, e, jv, rel);
+    int cell;
+    float w[16];
+    if (!grid_cell<4>(P.val, rel, cell, w)) {
+      gk = __builtin_nanf("");
+    } else if (k < 4) {
+      const GAS float* gc = (const GAS float*)(gptr(P.val.gcells) + (size_t)cell * 16) + k;
+      float gv[16];
+#pragma unroll
+      for (int c = 0; c < 16; ++c) gv[c] = gc[4 * c];
+#pragma unroll
+      for (int c = 0; c < 16; ++c) gk = gk + w[c] * gv[c];
+    }
+  }
+  float word = k < 4 ? gk : (k == 4 ? 0.0f : (k == 5 ? vmin : __int_as_float(k == 6 ? jv : st)));
+  filter_slot(S, N, e)[k] = word;
 }
 
 // Phase B of the team kernel: filter_agent with the slot filter_prep filled.
@@ -2415,7 +2507,8 @@ __device__ __forceinline__ void rk45_di_pair(double& p, double& v, double a, dou
   const double d1 = rk_norm4_pair(v / scp, a / scv, up);
   double h0 = (d0 < 1e-5 || d1 < 1e-5) ? 1e-6 : 0.01 * d0 / d1;
   h0 = (tb < h0) ? tb : h0;
-  const double d2 = rk_norm4_pair(((v + h0 * a) - v) / scp, (a - a) / scv, up) / h0;
+  // (a - a) / scv is +0 for the finite accelerations here (scv >= atol > 0): no division
+  const double d2 = rk_norm4_pair(((v + h0 * a) - v) / scp, (a - a) * 0.0, up) / h0;
   double h1;
   if (d1 <= 1e-15 && d2 <= 1e-15) {
     h1 = (h0 * 1e-3 > 1e-6) ? h0 * 1e-3 : 1e-6;
@@ -2492,13 +2585,13 @@ __device__ __forceinline__ void integrate_agent_di_pair(const KParams& P, Lds& S
   double q = lane32_partner(v);
   double sx = up ? q : v, sy = up ? v : q;
   double spd = sqrt(sx * sx + sy * sy);
-  if (spd > P.max_speed) {
+  if (spd > P.max_speed) {   // unclamped, the second norm is the first (the same operands)
     v = P.max_speed * v / spd;
     q = lane32_partner(v);
     sx = up ? q : v;
     sy = up ? v : q;
+    spd = sqrt(sx * sx + sy * sy);
   }
-  spd = sqrt(sx * sx + sy * sy);
   S.ps[c * N + i] = p;
   S.ps[(2 + c) * N + i] = v;
   if (!up) S.pdist[i] += spd * P.dt;
@@ -3497,7 +3590,12 @@ static void fill_params(const lsm_env* e, KParams& P) {
       P.act1[k] = (k == 4) ? ahi : alo + k * ((ahi - alo) / 4);
     }
   }
-  P.coord_range2 = P.coord_range * P.coord_range;
+  {
+    double t = P.coord_range * P.coord_range;
+    while (std::sqrt(t) > P.coord_range) t = std::nextafter(t, 0.0);
+    while (std::sqrt(std::nextafter(t, INFINITY)) <= P.coord_range) t = std::nextafter(t, INFINITY);
+    P.coord_range_s = t;
+  }
   P.cos_pi6 = cos(pi / 6);
   for (int k = 0; k < 50; ++k) {
     const double ph = k * ((2 * pi - 0) / 50);   // np.linspace(0, 2pi, 50, endpoint=False)
@@ -3787,6 +3885,32 @@ static int upload_table(lsm_env* e, TableDev& T, int32_t ndim, const double* lo,
     const double sp = T.periodic[d] ? (hi[d] - lo[d]) / shape[d] : (hi[d] - lo[d]) / (shape[d] - 1.0);
     T.lo[d] = (float)lo[d];
     T.sp[d] = (float)sp;
+  }
+  // grid_pos's reciprocal path, per dimension, where it equals the division for every y = s - lo
+  // a lookup can meet: grid positions within [-4, n + 3] (non-periodic: outside, the lookup is out
+  // of the grid either way -- a faithful quotient cannot cross those bounds) or within 1e9 in
+  // magnitude (periodic: the wrap reads the position itself; beyond 1e9 grid_cell refuses it)
+  {
+    int* bad = nullptr;
+    HIPCHK(e, hipMalloc((void**)&bad, sizeof(int)));
+    for (int d = 0; d < ndim; ++d) {
+      T.rsp[d] = 1.0f / T.sp[d];
+      T.mdiv[d] = 0;
+      if (!(T.sp[d] > 0.0f) || getenv("LSM_NO_MDIV")) continue;
+      const float plo = T.periodic[d] ? -1.0e9f : -4.0f;
+      const float phi = T.periodic[d] ? 1.0e9f : (float)(T.n[d] + 3);
+      const float ypos = phi * T.sp[d] * 1.0001f, yneg = -plo * T.sp[d] * 1.0001f;
+      uint32_t pb, nb;
+      memcpy(&pb, &ypos, 4);
+      memcpy(&nb, &yneg, 4);
+      HIPCHK(e, hipMemset(bad, 0, sizeof(int)));
+      hipLaunchKernelGGL(mdiv_check_kernel, dim3(4096), dim3(256), 0, 0, T.sp[d], T.rsp[d], pb, nb, bad);
+      HIPCHK(e, hipGetLastError());
+      int h = 1;
+      HIPCHK(e, hipMemcpy(&h, bad, sizeof(int), hipMemcpyDeviceToHost));
+      T.mdiv[d] = h == 0 ? 1 : 0;
+    }
+    HIPCHK(e, hipFree(bad));
   }
   const size_t ncorner = (size_t)1 << ndim;
   if (cells * ncorner * 2 > (size_t)INT32_MAX) return fail(e, "table too large for 32-bit cell offsets");

@@ -507,7 +507,9 @@ void rollout_team_kernel(const KParams* __restrict__ Pp, const KStep K) {
         const int j = p / N, i = p - j * N;   // [j][i]: ego i fastest (bank-conflict-free reads)
         if (i == j || S.dpre[i] || S.dpre[j]) continue;
         const double ex = S.ps[i], ey = S.ps[N + i], ox = S.ps[j], oy = S.ps[N + j];
-        S.dpair[p] = sqrt((ox - ex) * (ox - ex) + (oy - ey) * (oy - ey));
+        const double sq = (ox - ex) * (ox - ex) + (oy - ey) * (oy - ey);
+        // filter_prep_oct (DI, N = 8) works on squared distances (KParams::coord_range_s)
+        S.dpair[p] = (DYN == 0 && NT == 8) ? sq : sqrt(sq);
         double rel[5];
         rel_state<DYN>(S, N, i, j, rel);
         float v = 0.0f;
@@ -521,7 +523,8 @@ void rollout_team_kernel(const KParams* __restrict__ Pp, const KStep K) {
       // the deconflicting choice and the HJ gradient lookup of every ego, here where the other
       // waves of the SIMD hide the gather; the agent wave does the QP in B (filter_agent_slot)
       esync<LPE>();
-      if (lane < N) filter_prep<DYN, NT>(P, S, lane);
+      if (DYN == 0 && NT == 8) filter_prep_oct<8>(P, S);   // 32.66 -> 32.28 us (profiles/r05_v5_ab_c3_oct.txt)
+      else if (lane < N) filter_prep<DYN, NT>(P, S, lane);
       TSTAMP(17);
     }
   }
