@@ -43,7 +43,8 @@
 // variant builds (lsm.build.build_variants defines LSM_DIAGNOSTIC_BUILD); the product refuses them.
 #if !defined(LSM_DIAGNOSTIC_BUILD) &&                                                              \
     (defined(LSM_STAMPS) || defined(LSM_XP_VALHOT) || defined(LSM_XP_GRADHOT) || defined(LSM_XP_NOFILT) || \
-     defined(LSM_XP_NOOUT) || defined(LSM_XP_NORESETEMIT) || defined(LSM_XP_NORK) || defined(LSM_XP_NOSCEN))
+     defined(LSM_XP_NOOUT) || defined(LSM_XP_NORESETEMIT) || defined(LSM_XP_NORK) || defined(LSM_XP_NOSCEN) || \
+     defined(LSM_XP_DELAY))
 #error "diagnostic switch in a product build: use lsm.build.build_variants (LSM_DIAGNOSTIC_BUILD)"
 #endif
 
@@ -1951,8 +1952,9 @@ __device__ __forceinline__ void compute_dist(const KParams& P, Lds& S, const uin
     // specialised kernels preload this lane's pair words with the record (prw)
     const uint32_t pr = (NT && prw && t < nmov) ? prw[(t - lane) / LPE] : (uint32_t)gptr(P.pairs)[t];
     const int a = (int)(pr & 0xffu), b = (int)(pr >> 8);
-    const double xa = a < N ? S.ps[a] : S.lm[a - N];
-    const double ya = a < N ? S.ps[N + a] : S.lm[NL + a - N];
+    // a pair with an agent has it first (a < N): a step (not `full`) reads agent a directly
+    const double xa = (!full || a < N) ? S.ps[a] : S.lm[a - N];
+    const double ya = (!full || a < N) ? S.ps[N + a] : S.lm[NL + a - N];
     const double xb = b < N ? S.ps[b] : S.lm[b - N];
     const double yb = b < N ? S.ps[N + b] : S.lm[NL + b - N];
     const double dx = xa - xb, dy = ya - yb;

@@ -60,6 +60,17 @@ __host__ __device__ inline size_t team_env_bytes(size_t bytes, int N) {
 #define TSTAMP(k) do { } while (0)
 #define TRTSTAMP(k) do { } while (0)
 #endif
+// Diagnostic builds: LSM_XP_DELAY=p sleeps ~3000 cycles in phase p (1 A's env waves, 2 B's agent
+// wave, 3 C's env waves, 4 D's agent wave, 5 E's waves) -- how much of each phase lies on the path
+// to the end of the launch (same results, slower). Never in the product library.
+#if defined(LSM_XP_DELAY)
+#define XDELAY(p)                                                                                  \
+  do {                                                                                             \
+    if (LSM_XP_DELAY == (p)) __builtin_amdgcn_s_sleep(47);                                         \
+  } while (0)
+#else
+#define XDELAY(p) do { } while (0)
+#endif
 
 // ---- resets: the scenario draws ------------------------------------------------------------
 // random_scenario is a long scalar sequence (rejection loops, atan2, ~120 MT19937 doubles at N =
@@ -536,6 +547,7 @@ void rollout_team_kernel(const KParams* __restrict__ Pp, const KStep K) {
       else if (q < 320) ((f32x4*)carve(smem + B, N, NL, E, F, false).fval)[q - 192] = ptq[r];
     }
   }
+  XDELAY(1);
   TSTAMP(6);
   TSTOP(3);
   __syncthreads();
@@ -555,6 +567,7 @@ void rollout_team_kernel(const KParams* __restrict__ Pp, const KStep K) {
     }
   }
   if (w == WB) {
+    XDELAY(2);
     if (alane) filter_agent_slot<DYN, NT>(P, A, N, ai, A.cur[C_FILT] != 0.0);
     esync<LPE>();   // every filter of the env has read the pre-step state
     TSTAMP(9);
@@ -610,8 +623,8 @@ void rollout_team_kernel(const KParams* __restrict__ Pp, const KStep K) {
       esync<LPE>();
       magnetic_partials_wave<LPE, NT>(P, S, S.dpair, tab);
     }
-    m_pre = chunked ? ego_mask(S, N, L, -1) : 0;
   }
+  XDELAY(3);
   TSTAMP(7);
   __syncthreads();
   TSTAMP(3);
@@ -622,6 +635,7 @@ void rollout_team_kernel(const KParams* __restrict__ Pp, const KStep K) {
   // phase E then rewrites it). WD stores its own in E. (Splitting WD's env's egos over the other
   // waves in D was measured slower: 36.6 vs 34.5 us at config 3, G = 4.)
   if (w == WD) {
+    XDELAY(4);
     AgentTmp at;
     if (alane) {
       min_relative(A, N, ai);
@@ -648,6 +662,9 @@ void rollout_team_kernel(const KParams* __restrict__ Pp, const KStep K) {
       episode_stats<DYN>(P, A, N, ai);
     }
   } else if (live && chunked) {
+    // the disconnect mask before this step's updates, here rather than at the end of C (phase C
+    // is on the path to the first stores; these waves wait for the agent wave in D)
+    m_pre = ego_mask(S, N, L, -1);
 #ifndef LSM_XP_NOOUT   // diagnostic bound only: no graph outputs
     emit_adj_uniform<LPE, NT>(P, S, env, m_pre, 0, N);
 #endif
@@ -660,6 +677,7 @@ void rollout_team_kernel(const KParams* __restrict__ Pp, const KStep K) {
   // ---- E. info rows, dones, then what the speculation did not cover, or the auto-reset --------
   __shared__ int team_rs[G];   // this step's auto-resets of the workgroup's envs
   bool rs = false;
+  XDELAY(5);
   if (live) {
     rec_copy<LPE>((const f32x4*)S.info, (GAS f32x4*)(gptr(P.o.info) + (size_t)env * N * LSM_INFO_FIELDS),
                   N * LSM_INFO_FIELDS / 2);
