@@ -146,9 +146,9 @@ def bench_edges(env, dev, reps=50):
     gbps = (read + written) / (ms * 1e-3) / 1e9
     return {"op": "GNNBase.process_adj (gnn.py:376-407) on the device", "envs": m, "graphs": B, "E": E,
             "nnz": nnz, "ms_per_call": ms, "algorithmic_bytes": read + written, "achieved_GBps": gbps,
-            "frac_hbm_peak": gbps / PEAK_HBM_GBPS, "note": "two kernels + hipcub scan + one 8-B D2H read "
-            "of nnz per call (the torch.nonzero sync); re-reads of the adjacency in the emit pass are "
-            "L2/MALL hits"}
+            "frac_hbm_peak": gbps / PEAK_HBM_GBPS, "note": "count kernel + hipcub scan + emit kernel back to back "
+            "(emit reads nnz on the device), then one 8-B D2H read of nnz per call (the torch.nonzero "
+            "sync); re-reads of the adjacency in the emit pass are L2/MALL hits"}
 
 
 def cpu_share():

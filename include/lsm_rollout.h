@@ -295,8 +295,12 @@ int lsm_host_scenario(const lsm_config* cfg, const lsm_curriculum* cur, uint32_t
  * `masks` = [B][ceil(E/64)] (LSM_OUT_ADJ / LSM_OUT_ADJ_MASK of an LSM_ADJ_COMPACT handle); the
  * per-ego matrix is expanded on the fly. Two calls, like torch.nonzero's count-then-fill:
  *   lsm_edges_count  offsets int64 [B+1] (offsets[B] = nnz), device; needs a device workspace of
- *                    lsm_edges_workspace_bytes(B) bytes
+ *                    lsm_edges_workspace_bytes(B) bytes (scratch, cleared by the call itself)
  *   lsm_edges_emit   fills edge_index / edge_attr given nnz (= offsets[B], read by the caller)
+ *   lsm_edges_emit_dev  the same without the host round trip: nnz is read on the device from
+ *                    offsets[B]; edge_index holds 2*cap int64 and edge_attr cap floats (cap >= nnz,
+ *                    e.g. B*E*E), filled as [2][nnz] / [nnz][1] from their start; nothing is
+ *                    written when nnz > cap (the caller checks offsets[B] afterwards)
  * Errors: nonzero return, text in lsm_edges_last_error() (per host thread). */
 size_t lsm_edges_workspace_bytes(int64_t B);
 int lsm_edges_count(const float* adj, const uint64_t* masks, int64_t B, int32_t E, int32_t N,
@@ -304,6 +308,9 @@ int lsm_edges_count(const float* adj, const uint64_t* masks, int64_t B, int32_t 
 int lsm_edges_emit(const float* adj, const uint64_t* masks, int64_t B, int32_t E, int32_t N,
                    const int64_t* offsets, int64_t nnz, int64_t* edge_index, float* edge_attr,
                    void* hip_stream);
+int lsm_edges_emit_dev(const float* adj, const uint64_t* masks, int64_t B, int32_t E, int32_t N,
+                       const int64_t* offsets, int64_t cap, int64_t* edge_index, float* edge_attr,
+                       void* hip_stream);
 const char* lsm_edges_last_error(void);
 
 /* ---- Buffer insert: the derived rows of GMPERunner.insert / warmup (lsm_buffer.hip) ----------

@@ -20,7 +20,9 @@
 //                       count pass) and writes its edges at offsets[b] in row-major order; the
 //                       in-chunk position is the popcount of the ballot below the lane (mbcnt), so
 //                       the output order is exactly nonzero()'s; edges are compacted in LDS and
-//                       stored by consecutive lanes.
+//                       stored by consecutive lanes. The _dev entry reads nnz = offsets[B] on the
+//                       device (outputs sized by an upper bound), so the three launches run back to
+//                       back with the one host sync after all of them.
 // A graph's E*E values are walked as one flat index k = r*E + c in 64-lane chunks (4 elements per
 // lane with one 16-B load when E is even), so every lane is busy whatever E is (E = 24 rows would
 // leave 40 of 64 lanes idle per row).
@@ -129,15 +131,21 @@ __global__ __launch_bounds__(256) void edge_count_kernel(AdjSrc s, int64_t* __re
 // exclusive-prefix slot), then written out by consecutive lanes: every store instruction covers
 // consecutive edge slots (full 512-B / 256-B lines), where storing straight from the lane that found
 // the edge would scatter each instruction over partial lines.
+// nnz < 0: read it on the device (offsets[B]); the outputs then hold `cap` edges, and nothing is
+// written when nnz > cap (the caller sees nnz and reports it).
 template <int VEC>
 __global__ __launch_bounds__(256) void edge_emit_kernel(AdjSrc s, const int64_t* __restrict__ offsets,
-                                                        int64_t nnz, int64_t* __restrict__ edge_index,
+                                                        int64_t nnz, int64_t cap, int64_t* __restrict__ edge_index,
                                                         float* __restrict__ edge_attr) {
   __shared__ int32_t sk[GRAPHS_PER_BLOCK][WAVE * VEC];
   __shared__ float sv[GRAPHS_PER_BLOCK][WAVE * VEC];
   const int w = threadIdx.x >> 6;
   const int64_t b = (int64_t)blockIdx.x * GRAPHS_PER_BLOCK + w;
   if (b >= s.B) return;
+  if (nnz < 0) {
+    nnz = offsets[s.B];
+    if (nnz > cap) return;
+  }
   const float* g = graph_ptr(s, b);
   const uint64_t* m = s.masks ? s.masks + b * s.W : nullptr;
   const int EE = s.E * s.E;
@@ -261,10 +269,29 @@ int lsm_edges_emit(const float* adj, const uint64_t* masks, int64_t B, int32_t E
   if (B == 0 || nnz == 0) return 0;
   const int64_t blocks = (B + GRAPHS_PER_BLOCK - 1) / GRAPHS_PER_BLOCK;
   if (E % 2 == 0)
-    edge_emit_kernel<4><<<dim3((unsigned)blocks), 256, 0, (hipStream_t)stream>>>(s, offsets, nnz, edge_index,
+    edge_emit_kernel<4><<<dim3((unsigned)blocks), 256, 0, (hipStream_t)stream>>>(s, offsets, nnz, nnz, edge_index,
                                                                                  edge_attr);
   else
-    edge_emit_kernel<1><<<dim3((unsigned)blocks), 256, 0, (hipStream_t)stream>>>(s, offsets, nnz, edge_index,
+    edge_emit_kernel<1><<<dim3((unsigned)blocks), 256, 0, (hipStream_t)stream>>>(s, offsets, nnz, nnz, edge_index,
+                                                                                 edge_attr);
+  return hipGetLastError() == hipSuccess ? 0 : fail("launch failed");
+}
+
+int lsm_edges_emit_dev(const float* adj, const uint64_t* masks, int64_t B, int32_t E, int32_t N,
+                       const int64_t* offsets, int64_t cap, int64_t* edge_index, float* edge_attr,
+                       void* stream) {
+  AdjSrc s;
+  if (make_src(adj, masks, B, E, N, &s)) return 1;
+  if (!offsets) return fail("offsets is null");
+  if (cap < 0) return fail("cap < 0");
+  if (cap > 0 && (!edge_index || !edge_attr)) return fail("edge_index / edge_attr is null");
+  if (B == 0 || cap == 0) return 0;
+  const int64_t blocks = (B + GRAPHS_PER_BLOCK - 1) / GRAPHS_PER_BLOCK;
+  if (E % 2 == 0)
+    edge_emit_kernel<4><<<dim3((unsigned)blocks), 256, 0, (hipStream_t)stream>>>(s, offsets, -1, cap, edge_index,
+                                                                                 edge_attr);
+  else
+    edge_emit_kernel<1><<<dim3((unsigned)blocks), 256, 0, (hipStream_t)stream>>>(s, offsets, -1, cap, edge_index,
                                                                                  edge_attr);
   return hipGetLastError() == hipSuccess ? 0 : fail("launch failed");
 }

@@ -55,9 +55,9 @@
 #define LSM_HOST_PART 1
 #endif
 
-// stamps per env in LSM_OUT_DEBUG_STAMPS: 16 in the ABI; diagnostic builds stamp 32
+// stamps per env in LSM_OUT_DEBUG_STAMPS: 16 in the ABI; diagnostic builds stamp 40
 #ifdef LSM_STAMPS
-#define LSM_NSTAMP 32
+#define LSM_NSTAMP 40
 #else
 #define LSM_NSTAMP 16
 #endif
@@ -1317,7 +1317,7 @@ __device__ __forceinline__ void filter_prep(const KParams& P, Lds& S, int i) {
 // summation order; lanes k write word k of the ego's slot. Same slots as filter_prep on 8 lanes,
 // about a third fewer vector instructions for the wave.
 template <int NT>
-__device__ __forceinline__ void filter_prep_oct(const KParams& P, Lds& S) {
+__device__ __forceinline__ void filter_prep_oct(const KParams& P, Lds& S, GAS unsigned long long* stp = nullptr) {
   constexpr int DYN = 0;
   static_assert(NT == 8, "8 egos x 8 candidate lanes");
   LSM_DIMS;
@@ -1346,6 +1346,9 @@ __device__ __forceinline__ void filter_prep_oct(const KParams& P, Lds& S) {
     jv = tv ? ojv : jv;
     in = tv ? oin : in;
   }
+#ifdef LSM_STAMPS
+  if (lane == 0 && stp) stp[32] = __builtin_amdgcn_s_memtime();
+#endif
   int st = 0;
   if (eact) st = jd == 64 ? 1 : ((!(d > P.coord_range_s) && in) ? 3 : 2);
   if (st < 2) jv = -1;

@@ -514,6 +514,7 @@ void rollout_team_kernel(const KParams* __restrict__ Pp, const KStep K) {
     filter_on = S.cur[C_FILT] != 0.0;
     if (filter_on) {
       const SepChain sc = sep_chain(S.sep, P.s, env);
+      TSTAMP(30);
       for (int p = lane; p < N * N; p += LPE) {
         const int j = p / N, i = p - j * N;   // [j][i]: ego i fastest (bank-conflict-free reads)
         if (i == j || S.dpre[i] || S.dpre[j]) continue;
@@ -534,7 +535,12 @@ void rollout_team_kernel(const KParams* __restrict__ Pp, const KStep K) {
       // the deconflicting choice and the HJ gradient lookup of every ego, here where the other
       // waves of the SIMD hide the gather; the agent wave does the QP in B (filter_agent_slot)
       esync<LPE>();
-      if (DYN == 0 && NT == 8) filter_prep_oct<8>(P, S);   // 32.66 -> 32.28 us (profiles/r05_v5_ab_c3_oct.txt)
+#ifdef LSM_STAMPS
+      GAS unsigned long long* ostp = gptr(P.stamps) && live ? gptr(P.stamps) + (size_t)env * LSM_NSTAMP : nullptr;
+#else
+      GAS unsigned long long* ostp = nullptr;
+#endif
+      if (DYN == 0 && NT == 8) filter_prep_oct<8>(P, S, ostp);   // 32.66 -> 32.28 us (profiles/r05_v5_ab_c3_oct.txt)
       else if (lane < N) filter_prep<DYN, NT>(P, S, lane);
       TSTAMP(17);
     }

@@ -33,7 +33,7 @@ INFO_FIELDS = ("individual_reward", "min_relative_distance", "Dist_to_goal", "Ti
 EXPORTED = ("lsm_create", "lsm_destroy", "lsm_last_error", "lsm_set_value_table", "lsm_set_ttr_table",
             "lsm_bind_output", "lsm_output_bytes", "lsm_reset", "lsm_step", "lsm_num_entities",
             "lsm_node_features", "lsm_obs_dim", "lsm_host_mt_uniforms", "lsm_host_scenario",
-            "lsm_set_agent_state", "lsm_edges_workspace_bytes", "lsm_edges_count", "lsm_edges_emit",
+            "lsm_set_agent_state", "lsm_edges_workspace_bytes", "lsm_edges_count", "lsm_edges_emit", "lsm_edges_emit_dev",
             "lsm_edges_last_error", "lsm_bind_output_ring", "lsm_select_ring", "lsm_buffer_insert",
             "lsm_buffer_last_error", "lsm_host_rk45_di", "lsm_host_glibc_pow", "lsm_action_errors",
             "lsm_kernel_name", "lsm_reset_layout", "lsm_layout_doubles", "lsm_host_philox_uniforms",
@@ -93,6 +93,7 @@ def load_library(path: str = LIB_PATH):
         "lsm_edges_workspace_bytes": (SZ, [I64]),
         "lsm_edges_count": (I32, [P, P, I64, I32, I32, P, P, SZ, P]),
         "lsm_edges_emit": (I32, [P, P, I64, I32, I32, P, I64, P, P, P]),
+        "lsm_edges_emit_dev": (I32, [P, P, I64, I32, I32, P, I64, P, P, P]),
         "lsm_edges_last_error": (C.c_char_p, []),
         "lsm_bind_output_ring": (I32, [P, I32, P, SZ, I32, I32]),
         "lsm_select_ring": (I32, [P, I32]),

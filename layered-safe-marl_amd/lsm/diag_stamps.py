@@ -52,7 +52,7 @@ def main():
     n_envs = a.envs or c["envs"]
     env = GpuGraphVecEnv(args, num_envs=n_envs, device="cuda:0", value_table=vt, ttr_table=tt,
                          return_numpy=False, build_infos=False, adj_layout=c.get("adj_layout", "reference"))
-    stamps = torch.zeros((n_envs, 32), dtype=torch.int64, device="cuda:0")   # LSM_NSTAMP
+    stamps = torch.zeros((n_envs, 40), dtype=torch.int64, device="cuda:0")   # LSM_NSTAMP
     capi.check(env.lib.lsm_bind_output(env.h, capi.OUT_DEBUG_STAMPS, C.c_void_p(stamps.data_ptr()),
                                        stamps.numel() * 8), env.h)
     env.reset(4)
@@ -67,7 +67,7 @@ def main():
             hw = raw[:, 15].astype(np.uint64)   # HW_ID | XCC_ID << 32 of this step's waves
             s = raw.astype(np.float64)
             tstamps.append(s[:, :9].copy())
-            tstamps12.append(s[:, :32].copy())
+            tstamps12.append(s[:, :40].copy())
             stamps.zero_()
             acc.append(np.diff(s[:, [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10]], axis=1))
             t0 = s[:, 13].min()
@@ -98,6 +98,8 @@ def main():
               "  %10.2f  slots %s" % (np.median(rts[late]) / 1e3, np.bincount(slots[late], minlength=G).tolist()))
         ag = np.concatenate(tstamps12, axis=0)
         for name, i, j in [("A record", 0, 12), ("A decode+pairs", 12, 16), ("A argmin+grad", 16, 17),
+                           ("A: to pair loop", 12, 30), ("A: pair loop", 30, 16), ("A: argmins", 16, 32),
+                           ("A: gradient", 32, 17),
                            ("A decode..prep", 12, 6), ("B filter", 1, 9),
                            ("B integrate", 9, 2), ("B: to RK45 start", 9, 29), ("B: initial step", 29, 27),
                            ("B: RK45 steps", 27, 28), ("B: clamp+sync", 28, 2), ("D reward", 3, 10),

@@ -7,8 +7,10 @@ reference's GNN consumes. ``process_adj_compact(A, masks, N)`` does the same for
 (``LSM_ADJ_COMPACT``: one ``[n, E, E]`` table + per-ego disconnect masks), expanding each ego's
 matrix on the fly instead of materialising ``(n, N, E, E)``.
 
-Like ``torch.nonzero`` the call synchronises once (the edge count sizes the outputs). All work runs
-in ``lsm_edges.hip`` through the C ABI; there is no torch/CPU fallback.
+Like ``torch.nonzero`` the call synchronises once (the edge count sizes the outputs): after both
+kernels when the upper bound B*E*E of the outputs fits BOUNDED_OUTPUT_BYTES (the results are then
+contiguous views of those buffers), else between them. All work runs in ``lsm_edges.hip`` through
+the C ABI; there is no torch/CPU fallback.
 """
 from __future__ import annotations
 
@@ -31,6 +33,12 @@ def _check(rc, lib):
         raise EdgeError(lib.lsm_edges_last_error().decode())
 
 
+# outputs sized by the edge-count upper bound B*E*E up to this many bytes: count and emit then run back
+# to back and the call synchronises once, after both (the returned tensors are views of the
+# bounded buffers); above it the count is read first and the outputs are sized exactly
+BOUNDED_OUTPUT_BYTES = 4 << 30
+
+
 def _run(adj, masks, B, E, N):
     torch = _torch()
     lib = capi.load_library()
@@ -42,15 +50,25 @@ def _run(adj, masks, B, E, N):
     ws_bytes = int(lib.lsm_edges_workspace_bytes(B))
     ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
     mp = C.c_void_p(masks.data_ptr()) if masks is not None else None
-    _check(lib.lsm_edges_count(C.c_void_p(adj.data_ptr()), mp, B, E, N, C.c_void_p(offsets.data_ptr()),
-                               C.c_void_p(ws.data_ptr()), ws_bytes, stream), lib)
+    ap = C.c_void_p(adj.data_ptr())
+    _check(lib.lsm_edges_count(ap, mp, B, E, N, C.c_void_p(offsets.data_ptr()), C.c_void_p(ws.data_ptr()),
+                               ws_bytes, stream), lib)
+    cap = B * E * E
+    if 0 < cap * 20 <= BOUNDED_OUTPUT_BYTES:
+        ebuf = torch.empty(2 * cap, dtype=torch.int64, device=dev)
+        abuf = torch.empty(cap, dtype=torch.float32, device=dev)
+        _check(lib.lsm_edges_emit_dev(ap, mp, B, E, N, C.c_void_p(offsets.data_ptr()), cap,
+                                      C.c_void_p(ebuf.data_ptr()), C.c_void_p(abuf.data_ptr()), stream), lib)
+        nnz = int(offsets[B].item())   # the one sync, as in torch.nonzero (after both kernels)
+        if nnz > cap:
+            raise EdgeError("edge count %d exceeds B*E*E = %d" % (nnz, cap))
+        return ebuf[:2 * nnz].view(2, nnz), abuf[:nnz].view(nnz, 1)
     nnz = int(offsets[B].item())   # the one sync, as in torch.nonzero
     edge_index = torch.empty((2, nnz), dtype=torch.int64, device=dev)
     edge_attr = torch.empty((nnz, 1), dtype=torch.float32, device=dev)
     if nnz:
-        _check(lib.lsm_edges_emit(C.c_void_p(adj.data_ptr()), mp, B, E, N, C.c_void_p(offsets.data_ptr()),
-                                  nnz, C.c_void_p(edge_index.data_ptr()), C.c_void_p(edge_attr.data_ptr()),
-                                  stream), lib)
+        _check(lib.lsm_edges_emit(ap, mp, B, E, N, C.c_void_p(offsets.data_ptr()), nnz,
+                                  C.c_void_p(edge_index.data_ptr()), C.c_void_p(edge_attr.data_ptr()), stream), lib)
     return edge_index, edge_attr
 
 
