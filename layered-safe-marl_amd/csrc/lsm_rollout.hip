@@ -1081,14 +1081,16 @@ __device__ __forceinline__ void magnetic_partials_wave(const KParams& P, const L
       const double r0 = x - 0.0, r1 = y - Ly, r2 = 0.0 - Lz;
       const double c0 = dLy * r2 - dLz * r1;
       const double c1 = dLz * r0 - 0.0 * r2;
-      // 1 / |r|**3 from v_rsq_f64 (~2^-23 relative) and two Newton steps (~1 ulp), then two
-      // multiplies: a few ulp per term instead of ~1.5, no division (|r| > 0: r0 = x != 0).
-      // Round 3 took sqrt, rn**3 and two float64 divisions: 33.08 vs 31.82 us per step at config 2
-      // (profiles/r04_v2_ab_c2_mag.txt).
+      // 1 / |r|**3 from v_rsq_f64 (~2^-23 relative) and Newton steps, then two multiplies, no
+      // division (|r| > 0: r0 = x != 0). Round 3 took sqrt, rn**3 and two float64 divisions:
+      // 33.08 vs 31.82 us per step at config 2 (profiles/r04_v2_ab_c2_mag.txt). LSM_MAG_NEWTON1:
+      // one step (~2^-45 relative per term, far inside the reward tolerance) instead of two
       const double sq = fma(r2, r2, fma(r1, r1, r0 * r0));
       double ri = __builtin_amdgcn_rsq(sq);
       ri = fma(0.5 * ri, fma(-sq * ri, ri, 1.0), ri);
+#ifndef LSM_MAG_NEWTON1
       ri = fma(0.5 * ri, fma(-sq * ri, ri, 1.0), ri);
+#endif
       const double i3 = ri * ri * ri;
       m0 = fma(c0, i3, m0);
       m1 = fma(c1, i3, m1);
