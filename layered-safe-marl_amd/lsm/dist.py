@@ -95,21 +95,32 @@ class EpisodeSummaryReducer:
         # it is the row count of each submitted ep_info (n_local for the rollout's LSM_OUT_EP_INFO)
         self.n_local = int(n_local)
         self._pending = []
+        self._free = []   # output buffers of read results, reused by later submits
+        self._fn = None   # lsm_episode_summary, resolved once
 
-    def submit(self, ep_info: torch.Tensor):
-        out = torch.empty(10, dtype=torch.float64, device=ep_info.device)
-        if ep_info.is_cuda:
-            # one native launch (lsm_metrics.hip): sums, count, min -- no host sync
-            import ctypes as C
+    def _summary_fn(self):
+        if self._fn is None:
             from . import capi
             lib = capi.load_library()
             if getattr(lib, "lsm_episode_summary", None) is None:
                 raise capi.LsmError("%s lacks lsm_episode_summary (a library older than lsm_metrics.hip)"
                                     % capi.LIB_PATH)
-            ep = ep_info.contiguous()
+            self._fn = lib.lsm_episode_summary
+        return self._fn
+
+    def submit(self, ep_info: torch.Tensor):
+        # at an episode boundary inside a timed loop the host work is one ctypes launch: the
+        # output buffer comes from the pool once a previous result has been read
+        out = self._free.pop() if self._free and self._free[-1].device == ep_info.device else \
+            torch.empty(10, dtype=torch.float64, device=ep_info.device)
+        if ep_info.is_cuda:
+            # one native launch (lsm_metrics.hip): sums, count, min -- no host sync
+            import ctypes as C
+            from . import capi
+            ep = ep_info if ep_info.is_contiguous() else ep_info.contiguous()
             st = torch.cuda.current_stream(ep.device).cuda_stream
-            if lib.lsm_episode_summary(C.c_void_p(ep.data_ptr()), int(ep.shape[0]), C.c_void_p(out.data_ptr()),
-                                       C.c_void_p(st)) != 0:
+            if self._summary_fn()(C.c_void_p(ep.data_ptr()), int(ep.shape[0]), C.c_void_p(out.data_ptr()),
+                                  C.c_void_p(st)) != 0:
                 raise capi.LsmError("lsm_episode_summary failed")
         else:   # host tensors (gloo tests on the CPU): the same sums with torch
             torch.sum(ep_info, dim=0, out=out[:8])
@@ -121,16 +132,17 @@ class EpisodeSummaryReducer:
             import torch.distributed as dist
             works = (dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True),
                      dist.all_reduce(mn, op=dist.ReduceOp.MIN, group=self.group, async_op=True))
-        self._pending.append((buf, mn, works))
+        self._pending.append((out, buf, mn, works))
 
     def results(self):
         out = []
-        for buf, mn, works in self._pending:
+        for full, buf, mn, works in self._pending:
             for w in works:
                 w.wait()
             mean = (buf[:8] / buf[8]).tolist()
             d = dict(zip(EPKEYS, mean))
             d["min_distance_min"] = float(mn.item())
             out.append(d)
+            self._free.append(full)
         self._pending = []
         return out

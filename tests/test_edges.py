@@ -180,3 +180,51 @@ def test_gpu_env_edge_list_full_size(layout):
         ref = env.reference_adj().reshape(-1, env.E, env.E).cpu().numpy()
         _assert_same((ei.cpu().numpy(), ea.cpu().numpy()), ora_process_adj(ref))
     env.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,E", [(1000, 24), (33, 192), (7, 9)])
+def test_gpu_process_adj_bounded_and_exact_paths_agree(B, E):
+    """The one-sync path (outputs sized by B*E*E, nnz read on the device by the emit kernel) and the
+    count-first path (outputs sized exactly) give the same tensors, both equal to the oracle; the
+    bounded results are contiguous [2, nnz] / [nnz, 1] views."""
+    from lsm import edges
+    rng = np.random.default_rng(B * 3 + E)
+    a = _random_adj(rng, B, E)
+    want = ora_process_adj(a)
+    saved = edges.BOUNDED_OUTPUT_BYTES
+    try:
+        edges.BOUNDED_OUTPUT_BYTES = 4 << 30
+        ei, ea = edges.process_adj(_gpu(a))
+        assert ei.is_contiguous() and ea.is_contiguous()
+        _assert_same((ei.cpu().numpy(), ea.cpu().numpy()), want)
+        edges.BOUNDED_OUTPUT_BYTES = 0
+        _assert_same(_run_ref(a), want)
+    finally:
+        edges.BOUNDED_OUTPUT_BYTES = saved
+
+
+@pytest.mark.gpu
+def test_gpu_edges_emit_dev_writes_nothing_past_cap():
+    """lsm_edges_emit_dev with cap < nnz (offsets[B] read on the device) leaves the outputs untouched."""
+    import ctypes as C
+    import torch
+    from lsm import capi
+    lib = capi.load_library()
+    rng = np.random.default_rng(5)
+    a = _gpu(_random_adj(rng, 16, 24, density=0.8))
+    B, E = 16, 24
+    st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    off = torch.empty(B + 1, dtype=torch.int64, device="cuda:0")
+    wsb = int(lib.lsm_edges_workspace_bytes(B))
+    ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device="cuda:0")
+    assert lib.lsm_edges_count(C.c_void_p(a.data_ptr()), None, B, E, 1, C.c_void_p(off.data_ptr()),
+                               C.c_void_p(ws.data_ptr()), wsb, st) == 0
+    nnz = int(off[B].item())
+    cap = nnz // 2
+    ei = torch.full((2 * cap,), -7, dtype=torch.int64, device="cuda:0")
+    ea = torch.full((cap,), -7.0, dtype=torch.float32, device="cuda:0")
+    assert lib.lsm_edges_emit_dev(C.c_void_p(a.data_ptr()), None, B, E, 1, C.c_void_p(off.data_ptr()), cap,
+                                  C.c_void_p(ei.data_ptr()), C.c_void_p(ea.data_ptr()), st) == 0
+    torch.cuda.synchronize()
+    assert bool((ei == -7).all()) and bool((ea == -7.0).all())
