@@ -1075,25 +1075,30 @@ __device__ __forceinline__ void magnetic_partials_wave(const KParams& P, const L
   if (act && !(fabs(rpx) < 1e-6)) {
     const double x = 0.5 * rpx, y = rpy;
     const double nr = -radius;
-    for (int k = g; k < 50; k += G) {
+    // segments k and 50 - k (angles 2 pi k / 50 and 2 pi - 2 pi k / 50) contribute the same term:
+    // with the segment at (0, -R cos, -R sin) and tangent (0, R sin, -R cos), c0 = R^2 sin^2 +
+    // R cos (y + R cos), c1 = -R cos x and |r|^2 = x^2 + (y + R cos)^2 + R^2 sin^2 are even in sin.
+    // So k = 1 .. 24 count twice and 0, 25 once: 26 terms instead of 50 (the mirrored cos / sin
+    // values differ from these in the last bit only; ulp-level, like the rest of this sum).
+    // 28.47 -> 27.95 us per step at config 2 (profiles/r05_s27_ab_c2.txt)
+    for (int k = g; k <= 25; k += G) {
+      const double wk = (k == 0 || k == 25) ? 1.0 : 2.0;
       const double Ly = nr * mc[k], Lz = nr * ms[k];
       const double dLy = radius * ms[k], dLz = nr * mc[k];
       const double r0 = x - 0.0, r1 = y - Ly, r2 = 0.0 - Lz;
       const double c0 = dLy * r2 - dLz * r1;
       const double c1 = dLz * r0 - 0.0 * r2;
-      // 1 / |r|**3 from v_rsq_f64 (~2^-23 relative) and Newton steps, then two multiplies, no
-      // division (|r| > 0: r0 = x != 0). Round 3 took sqrt, rn**3 and two float64 divisions:
-      // 33.08 vs 31.82 us per step at config 2 (profiles/r04_v2_ab_c2_mag.txt). LSM_MAG_NEWTON1:
-      // one step (~2^-45 relative per term, far inside the reward tolerance) instead of two
+      // 1 / |r|**3 from v_rsq_f64 (~2^-23 relative) and two Newton steps (~1 ulp), then two
+      // multiplies: a few ulp per term, no division (|r| > 0: r0 = x != 0). Round 3 took sqrt, rn**3
+      // and two float64 divisions: 33.08 vs 31.82 us per step at config 2 (r04_v2_ab_c2_mag.txt);
+      // one Newton step measured no faster (r05_s27_ab_c2.txt)
       const double sq = fma(r2, r2, fma(r1, r1, r0 * r0));
       double ri = __builtin_amdgcn_rsq(sq);
       ri = fma(0.5 * ri, fma(-sq * ri, ri, 1.0), ri);
-#ifndef LSM_MAG_NEWTON1
       ri = fma(0.5 * ri, fma(-sq * ri, ri, 1.0), ri);
-#endif
       const double i3 = ri * ri * ri;
-      m0 = fma(c0, i3, m0);
-      m1 = fma(c1, i3, m1);
+      m0 = fma(wk * c0, i3, m0);
+      m1 = fma(wk * c1, i3, m1);
     }
   }
   part[lane] = m0;

@@ -468,31 +468,8 @@ void rollout_team_kernel(const KParams* __restrict__ Pp, const KStep K) {
     }
     // a plain step needs [0, a2) of the record before its distances; the rest (statistics,
     // landmarks) comes in phase B (cold_loads). Resets and the edge output read it all here.
-#ifdef LSM_AB_KPRE2
-    {
-      // the record's loads issued first, then one scalar load per 64-B line of the kernel
-      // parameters (folded and sunk) while they are in flight: the phases' later parameter reads
-      // then hit the scalar cache instead of L2 (one dependent L2 round trip each today)
-      const GAS f32x4* rs = (const GAS f32x4*)gptr(P.s.rec) + (size_t)env * P.s.rec_stride16;
-      const int rn = split ? P.s.a2_16 : P.s.rec16;
-      if (rn <= 2 * LPE) {
-        const int k0 = lane, k1 = lane + LPE;
-        const f32x4 r0 = rs[k0 < rn ? k0 : 0], r1 = rs[k1 < rn ? k1 : 0];
-        const int* kp = (const int*)Pp;
-        int acc = 0;
-#pragma unroll
-        for (int o = 0; o < (int)(sizeof(KParams) / 4); o += 16) acc ^= kp[o];
-        asm volatile("" ::"s"(acc));
-        if (k0 < rn) ((f32x4*)lbase)[k0] = r0;
-        if (k1 < rn) ((f32x4*)lbase)[k1] = r1;
-      } else {
-        rec_copy<LPE>(rs, (f32x4*)lbase, rn);
-      }
-    }
-#else
     rec_copy<LPE>((const GAS f32x4*)gptr(P.s.rec) + (size_t)env * P.s.rec_stride16, (f32x4*)lbase,
                   split ? P.s.a2_16 : P.s.rec16);
-#endif
     esync<LPE>();
     TSTAMP(12);
     TSTOP(1);
