@@ -20,8 +20,10 @@ KERN="lsm::rollout"
 
 run() {  # run <name> <rocprofv3 args...>
   local name=$1; shift
+  echo "$(date +%T) config $CFG: $name ..."   # progress on stdout (a gpurun_out log): no silent minutes
   (cd /tmp && timeout -k 10 300 rocprofv3 "$@" -d "$OUT/$name" -o run --output-format csv \
       -- python3 "$ROOT"/$BENCH > "$OUT/$name.log" 2>&1)
+  echo "$(date +%T) config $CFG: $name done"
 }
 
 run ktrace --kernel-trace --stats
