@@ -1,12 +1,10 @@
-"""Host cost of one GpuGraphVecEnv.step_async + step_wait (device tensors), i.e. how far ahead of
-the GPU the Python loop can enqueue. The loop runs K launches without synchronising (the launch
-queue absorbs them) and reports host microseconds per call, then the GPU time per step.
+"""DIAGNOSTIC: host-side cost of one GpuGraphVecEnv.step_async + step_wait at config 3 (4096 envs,
+filter on), and the idle time in front of the first launch of a window (what a 20-step driver window
+pays once): (1) host microseconds per call with the launch queue deep; (2) event time of one step
+launched onto an idle GPU, minus the kernel's own time from a back-to-back run.
 
-    python layered-safe-marl_amd/tools/host_overhead.py [--envs 4096] [--calls 400]
+    python layered-safe-marl_amd/tools/host_overhead.py
 """
-from __future__ import annotations
-
-import argparse
 import json
 import os
 import sys
@@ -14,35 +12,70 @@ import time
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(HERE))
+sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
 
 
 def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--envs", type=int, default=4096)
-    ap.add_argument("--calls", type=int, default=400)
-    a = ap.parse_args()
     import torch
+    import bench
     from lsm import hj_tables
-    from lsm.config import EnvArgs
     from lsm.vec_env import GpuGraphVecEnv
-    args = EnvArgs(num_agents=8, num_env_steps=250 * 4, use_safety_filter=True, seed=0)
+    c = bench.CONFIGS[3]
+    args = bench.make_args(c)
     vt, _ = hj_tables.default_tables("double_integrator")
-    env = GpuGraphVecEnv(args, num_envs=a.envs, device="cuda:0", value_table=vt, return_numpy=False)
+    env = GpuGraphVecEnv(args, num_envs=c["envs"], device="cuda:0", value_table=vt, return_numpy=False,
+                         build_infos=False)
     env.reset(4)
-    acts = torch.randint(0, 25, (a.calls, a.envs, 8), device="cuda:0", dtype=torch.int32)
-    for t in range(20):
-        env.step_async(acts[t], 4)
+    acts = torch.randint(0, 25, (c["envs"], c["num_agents"]), device="cuda:0", dtype=torch.int32)
+    for _ in range(20):
+        env.step_async(acts, 4)
         env.step_wait()
     torch.cuda.synchronize()
+    # (1) host time per call, queue deep (the GPU is the slower side)
+    n = 200
     t0 = time.perf_counter()
-    for t in range(a.calls):
-        env.step_async(acts[t], 4)
+    for _ in range(n):
+        env.step_async(acts, 4)
         env.step_wait()
-    t1 = time.perf_counter()
+    host_us = (time.perf_counter() - t0) / n * 1e6
     torch.cuda.synchronize()
-    t2 = time.perf_counter()
-    print(json.dumps({"envs": a.envs, "calls": a.calls, "host_us_per_call": (t1 - t0) * 1e6 / a.calls,
-                      "wall_us_per_step": (t2 - t0) * 1e6 / a.calls}))
+    # back-to-back kernel time
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(n):
+        env.step_async(acts, 4)
+    e1.record()
+    torch.cuda.synchronize()
+    b2b_us = e0.elapsed_time(e1) / n * 1e3
+    # (2) one step onto an idle GPU: event time from a marker recorded just before the call
+    one = []
+    for _ in range(50):
+        torch.cuda.synchronize()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        env.step_async(acts, 4)
+        b.record()
+        torch.cuda.synchronize()
+        one.append(a.elapsed_time(b) * 1e3)
+    one.sort()
+    # (3) the host cost of each part of step_async (no launch): curriculum lookup, action tensor,
+    # stream handle
+    t0 = time.perf_counter()
+    for _ in range(2000):
+        env._curriculum(4)
+    cur_us = (time.perf_counter() - t0) / 2000 * 1e6
+    t0 = time.perf_counter()
+    for _ in range(2000):
+        env._actions_device(acts)
+    act_us = (time.perf_counter() - t0) / 2000 * 1e6
+    t0 = time.perf_counter()
+    for _ in range(2000):
+        env._stream()
+    st_us = (time.perf_counter() - t0) / 2000 * 1e6
+    print(json.dumps({"host_us_per_step_queue_deep": host_us, "kernel_us_back_to_back": b2b_us,
+                      "idle_gpu_one_step_event_us_median": one[len(one) // 2], "min": one[0],
+                      "front_latency_us_median": one[len(one) // 2] - b2b_us,
+                      "host_us_curriculum": cur_us, "host_us_actions": act_us, "host_us_stream": st_us}))
     env.close()
 
 
