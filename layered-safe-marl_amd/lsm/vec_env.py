@@ -289,6 +289,13 @@ class GpuGraphVecEnv(ShareVecEnv):
 
     def _actions_device(self, actions):
         torch = _torch()
+        # fast path, no torch op calls: the runner's (n, N) int32 device tensor as it already is
+        # (each .to() / .contiguous() is a dispatcher round with device guards on the host; a
+        # 20-step window's first step paid ~100 us of host time before its launch:
+        # profiles/r05_s28_window_attrib.txt)
+        if isinstance(actions, torch.Tensor) and actions.dtype == torch.int32 and actions.dim() == 2 and \
+                actions.device == self.device and actions.is_contiguous():
+            return actions, capi.LSM_ACTIONS_INDEX_I32
         if isinstance(actions, torch.Tensor):
             t = actions.to(self.device)
         else:
