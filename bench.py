@@ -351,18 +351,24 @@ def main():
 
     summaries.submit(env.t_epinfo)   # load the reduction kernels / RCCL before any timed call
     summaries.results()
+    # No Python garbage collection inside the window: a collection pass stalls the host for ~0.1 ms,
+    # and with the launch queue that shallow the GPU idles (a 73 us gap in
+    # profiles/r05_v3_driver_window.txt). The collection runs before the untimed steps, so the
+    # memory it returns is taken up again by them, not by the window's first step.
+    # (the driver's 20-step window: 7.74-7.95e8 -> 8.60-9.27e8 agent-steps/s with this ordering and the
+    # events below, same session: profiles/r05_s31_*.json)
+    import gc
+    gc.collect()
+    gc.disable()
     for t in range(pre):
         one_step(t)
     summaries.results()
     # Kernel time: HIP events on the launch stream bracketing the whole timed region (per-launch
-    # event pairs would add their own GPU-side markers between back-to-back launches).
+    # event pairs would add their own GPU-side markers between back-to-back launches). Both are
+    # recorded once before the window: the HIP events are created at their first record.
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    # no Python garbage collection inside the window: a collection pass stalls the host for ~0.1 ms,
-    # and with the launch queue that shallow the GPU idles (a 73 us gap in
-    # profiles/r05_v3_driver_window.txt)
-    import gc
-    gc.collect()
-    gc.disable()
+    ev0.record()
+    ev1.record()
     torch.cuda.synchronize()
     barrier(a.dist_backend)
     torch.cuda.synchronize()
