@@ -3905,10 +3905,15 @@ static int upload_table(lsm_env* e, TableDev& T, int32_t ndim, const double* lo,
   {
     int* bad = nullptr;
     HIPCHK(e, hipMalloc((void**)&bad, sizeof(int)));
+#ifdef LSM_DIAGNOSTIC_BUILD
+    const bool no_mdiv = getenv("LSM_NO_MDIV") != nullptr;   // A/B of the division path (variant builds)
+#else
+    const bool no_mdiv = false;   // the product reads no environment knobs
+#endif
     for (int d = 0; d < ndim; ++d) {
       T.rsp[d] = 1.0f / T.sp[d];
       T.mdiv[d] = 0;
-      if (!(T.sp[d] > 0.0f) || getenv("LSM_NO_MDIV")) continue;
+      if (!(T.sp[d] > 0.0f) || no_mdiv) continue;
       const float plo = T.periodic[d] ? -1.0e9f : -4.0f;
       const float phi = T.periodic[d] ? 1.0e9f : (float)(T.n[d] + 3);
       const float ypos = phi * T.sp[d] * 1.0001f, yneg = -plo * T.sp[d] * 1.0001f;
