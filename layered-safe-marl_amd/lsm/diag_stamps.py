@@ -32,6 +32,9 @@ def main():
     ap.add_argument("--envs", type=int, default=0)
     ap.add_argument("--team", action="store_true",
                     help="the team kernel's stamps (lsm_team.h): phases A-E, work vs barrier wait")
+    ap.add_argument("--pick", default="",
+                    help="comma-separated step indices to keep (e.g. 250: the step after the first "
+                         "episode boundary at episode length 250); default every step from 10 on")
     a = ap.parse_args()
     if a.build or not os.path.exists(STAMP_LIB):
         build_stamps()
@@ -62,7 +65,8 @@ def main():
         act = torch.randint(0, 25, (n_envs, N), device="cuda:0", dtype=torch.int32)
         env.step(act, 4)
         torch.cuda.synchronize()
-        if t >= 10:
+        picks = {int(x) for x in a.pick.split(",") if x}
+        if (t >= 10 and not picks) or t in picks:
             raw = stamps.cpu().numpy()
             hw = raw[:, 15].astype(np.uint64)   # HW_ID | XCC_ID << 32 of this step's waves
             s = raw.astype(np.float64)
@@ -72,6 +76,8 @@ def main():
             acc.append(np.diff(s[:, [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10]], axis=1))
             t0 = s[:, 13].min()
             rt.append(np.stack([s[:, 13] - t0, s[:, 14] - t0], axis=1) * 10.0)   # ns (100 MHz)
+        else:
+            stamps.zero_()   # a picked step sees only its own stamps
     if a.team:
         # 0 start, 6 A done, 1 after W1, 2 after W2 (B), 7 C done, 3 after W3, 8 D done, 4 after W4, 5 end
         segs = [("A work", 0, 6), ("A wait", 6, 1), ("B (agent wave)", 1, 2), ("C work", 2, 7),
