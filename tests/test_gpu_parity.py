@@ -535,15 +535,16 @@ def test_gpu_runner_call_pattern_separation_curriculum(kernel, monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("kernel", ["wave", "block"])
+@pytest.mark.parametrize("kernel", ["wave", "block", "team"])
 def test_gpu_separation_chain_unbounded(kernel, monkeypatch):
     """HjDataHandle.update_separation_distance (safety_filter.py:170-174) has no limit: 24 separation
     changes (alternating stair levels, well past the record's 8 slots: the chain continues in the
     per-env HBM overflow, grown twice) and the filter after each still matches the oracle, whose
-    table is shifted in place as the reference's is; a re-upload then starts every chain afresh."""
+    table is shifted in place as the reference's is; a re-upload then starts every chain afresh.
+    "team": 8 agents, the config-3 kernel (rollout_team_kernel<0, 8, 4>)."""
     if kernel == "block":
         monkeypatch.setenv("LSM_KERNEL", "block")
-    meta = dict(dynamics_type="double_integrator", num_agents=4, num_landmarks=2, world_size=4,
+    meta = dict(dynamics_type="double_integrator", num_agents=8 if kernel == "team" else 4, num_landmarks=2, world_size=4,
                 episode_length=5, num_env_steps=5 * 20, n_rollout_threads=1, use_safety_filter=True,
                 use_masking=True, num_internal_step=1, seed=1, env_seed=1, separation_distance_curriculum=True)
     n = 3
@@ -568,7 +569,8 @@ def test_gpu_separation_chain_unbounded(kernel, monkeypatch):
                                           np.stack([e.deconflicting for e in ora.envs]), err_msg=ctx)
             np.testing.assert_array_equal(info[:, :, _info_col("Safety filtered")].astype(bool),
                                           np.stack([e.safety_filtered for e in ora.envs]), err_msg=ctx)
-    assert env.lib.lsm_kernel_name(env.h)
+    name = env.lib.lsm_kernel_name(env.h).decode()
+    assert ("team" in name) == (kernel == "team"), name
     env._upload_value_table()   # a new HjDataHandle: chains start empty, nothing refused
     env.reset(12)
     env.close()
