@@ -125,6 +125,16 @@ def test_gpu_process_adj_reference_layout(B, E):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("B,E", [(1023, 3), (1025, 3), (8193, 3), (32769, 2), (65536, 2), (65537, 2)])
+def test_gpu_process_adj_scan_sizes(B, E):
+    """Graph counts around 1024 / 8192 / 32 768 / 65 536 for the offsets scan (a one-workgroup scan
+    kernel was measured at these sizes against hipcub's and dropped, profiles/r05_s3{8,9}_*)."""
+    rng = np.random.default_rng(B)
+    a = _random_adj(rng, B, E)
+    _assert_same(_run_ref(a), ora_process_adj(a))
+
+
+@pytest.mark.gpu
 def test_gpu_process_adj_2d_empty_and_dense():
     rng = np.random.default_rng(1)
     a = _random_adj(rng, 1, 24)[0]
