@@ -148,7 +148,8 @@ def bench_edges(env, dev, reps=50):
             "nnz": nnz, "ms_per_call": ms, "algorithmic_bytes": read + written, "achieved_GBps": gbps,
             "frac_hbm_peak": gbps / PEAK_HBM_GBPS, "note": "count kernel + hipcub scan + emit kernel back to back "
             "(emit reads nnz on the device), then one 8-B D2H read of nnz per call (the torch.nonzero "
-            "sync); re-reads of the adjacency in the emit pass are L2/MALL hits"}
+            "sync); the emit pass re-reads the adjacency from beyond L2 (rocprofv3 FETCH_SIZE: the same ~75 MB as the "
+            "count pass at config 3, profiles/r05_s42_edges_traffic.txt), so both reads are counted"}
 
 
 def cpu_share():
