@@ -39,16 +39,36 @@ def _check(rc, lib):
 BOUNDED_OUTPUT_BYTES = 4 << 30
 
 
+# offsets + scan workspace of the last few (device, stream, B): reused by the next call with the same
+# key (stream-ordered: that call's count kernel runs after this call's emit kernel has read them), so a
+# call's host prologue before its first launch -- GPU idle time after the previous call's sync -- is
+# two ctypes launches instead of two allocations and a workspace query more
+_SCRATCH = {}
+
+
+def _scratch(lib, dev, stream_handle, B):
+    torch = _torch()
+    key = (dev.index, stream_handle, B)
+    hit = _SCRATCH.get(key)
+    if hit is None:
+        ws_bytes = int(lib.lsm_edges_workspace_bytes(B))
+        hit = (torch.empty(B + 1, dtype=torch.int64, device=dev),
+               torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev), ws_bytes)
+        if len(_SCRATCH) >= 8:
+            _SCRATCH.clear()
+        _SCRATCH[key] = hit
+    return hit
+
+
 def _run(adj, masks, B, E, N):
     torch = _torch()
     lib = capi.load_library()
     dev = adj.device
     if dev.type != "cuda":
         raise EdgeError("process_adj needs a CUDA (HIP) tensor; the edge list is built on the GPU")
-    stream = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
-    offsets = torch.empty(B + 1, dtype=torch.int64, device=dev)
-    ws_bytes = int(lib.lsm_edges_workspace_bytes(B))
-    ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
+    sh = torch.cuda.current_stream(dev).cuda_stream
+    stream = C.c_void_p(sh)
+    offsets, ws, ws_bytes = _scratch(lib, dev, sh, B)
     mp = C.c_void_p(masks.data_ptr()) if masks is not None else None
     ap = C.c_void_p(adj.data_ptr())
     _check(lib.lsm_edges_count(ap, mp, B, E, N, C.c_void_p(offsets.data_ptr()), C.c_void_p(ws.data_ptr()),
