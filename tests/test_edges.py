@@ -238,3 +238,30 @@ def test_gpu_edges_emit_dev_writes_nothing_past_cap():
                                   C.c_void_p(ei.data_ptr()), C.c_void_p(ea.data_ptr()), st) == 0
     torch.cuda.synchronize()
     assert bool((ei == -7).all()) and bool((ea == -7.0).all())
+
+
+def test_scratch_reuse_keys_and_bound():
+    """lsm.edges reuses the offsets / scan workspace per (device, stream, B) and keeps at most 8 keys
+    (host logic only: a stand-in for the workspace query, CPU tensors)."""
+    import torch
+    from lsm import edges
+
+    class _Lib:
+        calls = 0
+
+        def lsm_edges_workspace_bytes(self, B):
+            _Lib.calls += 1
+            return 64 * B + 256
+
+    lib, dev = _Lib(), torch.device("cpu")
+    edges._SCRATCH.clear()
+    o1, w1, n1 = edges._scratch(lib, dev, 0, 10)
+    o2, w2, n2 = edges._scratch(lib, dev, 0, 10)
+    assert o1 is o2 and w1 is w2 and n1 == n2 == 64 * 10 + 256 and _Lib.calls == 1
+    assert o1.shape == (11,) and o1.dtype == torch.int64 and w1.numel() == n1
+    assert edges._scratch(lib, dev, 1, 10)[0] is not o1      # another stream: its own buffers
+    assert edges._scratch(lib, dev, 0, 11)[0].shape == (12,)  # another graph count
+    for b in range(20, 40):
+        edges._scratch(lib, dev, 0, b)
+    assert len(edges._SCRATCH) <= 8
+    edges._SCRATCH.clear()
