@@ -114,42 +114,85 @@ def load_traffic(config, n_envs, build_id):
     return None
 
 
-def bench_edges(env, dev, reps=50):
-    """process_adj (count + scan + emit) over this GPU's n*N per-ego graphs of the last step.
-    Algorithmic bytes: the adjacency read twice (count and emit passes; compact: the table once per
-    ego graph + its mask words) + offsets + 16 B edge_index + 4 B edge_attr per edge."""
+def bench_edges(env, dev, step_fn, reps=50):
+    """process_adj (gnn.py:376-407) over this GPU's n*N per-ego graphs, two ways:
+    "count_pass": count kernel + hipcub scan + emit kernel on the last adjacency (the adjacency read
+    twice: the emit pass re-reads it from beyond L2, profiles/r05_s42_edges_traffic.txt);
+    "one_pass": the step kernel also writes each graph's nonzeros (LSM_OUT_ADJ_NNZ), and the call is
+    scan + emit (lsm_edges_scan_emit), the adjacency read once. step_fn(k) runs k more env steps; the
+    step time with and without the counts bound is measured alternately (what the counts cost the step).
+    Algorithmic bytes: adjacency reads (+ mask words, compact) + counts / offsets + 16 B edge_index + 4 B
+    edge_attr per edge. Each call includes its one 16-B (or 8-B) D2H read, the torch.nonzero sync."""
+    import ctypes as C
     import torch
-    from lsm import edges
+    from lsm import capi, edges
     E, N = env.E, env.N
     # at config 5 all 8192 x 64 per-ego graphs would be ~12 G edges (200 GiB): time the envs whose
     # worst-case edge list fits 16 GiB, as a learner consuming minibatches would
     m = max(1, min(env.num_envs, (16 << 30) // (N * E * E * 20)))
-    if env.t_adj_mask is None:
-        call = lambda: edges.process_adj(env.t_adj[:m].reshape(-1, E, E))
-    else:
-        call = lambda: edges.process_adj_compact(env.t_adj[:m], env.t_adj_mask[:m], N)
-    ei, ea = call()                                 # warm-up, allocates, loads kernels
-    nnz = ei.shape[1]
-    del ei, ea
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(reps):
-        call()
-    e1.record()
-    torch.cuda.synchronize()
-    ms = e0.elapsed_time(e1) / reps                 # includes the nnz host read-back per call
+    compact = env.t_adj_mask is not None
     B = m * N
     W = (E + 63) // 64
-    read = 2 * B * (E * E * 4 + (W * 8 if env.t_adj_mask is not None else 0))
-    written = nnz * 20 + (B + 1) * 8 + B * 8
-    gbps = (read + written) / (ms * 1e-3) / 1e9
-    return {"op": "GNNBase.process_adj (gnn.py:376-407) on the device", "envs": m, "graphs": B, "E": E,
-            "nnz": nnz, "ms_per_call": ms, "algorithmic_bytes": read + written, "achieved_GBps": gbps,
-            "frac_hbm_peak": gbps / PEAK_HBM_GBPS, "note": "count kernel + hipcub scan + emit kernel back to back "
-            "(emit reads nnz on the device), then one 8-B D2H read of nnz per call (the torch.nonzero "
-            "sync); the emit pass re-reads the adjacency from beyond L2 (rocprofv3 FETCH_SIZE: the same ~75 MB as the "
-            "count pass at config 3, profiles/r05_s42_edges_traffic.txt), so both reads are counted"}
+    adj_read = B * (E * E * 4 + (W * 8 if compact else 0))   # per ego graph (compact: its env's table + mask)
+
+    def run(counts):
+        if not compact:
+            return edges.process_adj(env.t_adj[:m].reshape(-1, E, E), counts=counts)
+        return edges.process_adj_compact(env.t_adj[:m], env.t_adj_mask[:m], N, counts=counts)
+
+    def timed(counts):
+        ei, ea = run(counts)                          # warm-up, allocates, loads kernels
+        nnz = ei.shape[1]
+        del ei, ea
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            run(counts)
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / reps, nnz
+
+    out = {"op": "GNNBase.process_adj (gnn.py:376-407) on the device", "envs": m, "graphs": B, "E": E}
+    ms, nnz = timed(None)
+    read = 2 * adj_read
+    written = nnz * 20 + (B + 2) * 8 + B * 8
+    out["count_pass"] = {"ms_per_call": ms, "nnz": nnz, "algorithmic_bytes": read + written,
+                         "achieved_GBps": (read + written) / (ms * 1e-3) / 1e9,
+                         "frac_hbm_peak": (read + written) / (ms * 1e-3) / 1e9 / PEAK_HBM_GBPS,
+                         "note": "count + scan + emit: the adjacency read twice (both reads counted)"}
+    if env.kernel_name.startswith("rollout_block_kernel"):
+        out["one_pass"] = None   # LSM_OUT_ADJ_NNZ: one-wave and team kernels (E <= 64)
+        return out
+    cnt = torch.zeros((env.num_envs, N), dtype=torch.int64, device=dev)
+
+    def bind(t):
+        capi.check(env.lib.lsm_bind_output(env.h, capi.OUT_ADJ_NNZ, C.c_void_p(t.data_ptr() if t is not None else 0),
+                                           t.numel() * 8 if t is not None else 0), env.h)
+
+    step_ms = {"with_counts": [], "without": []}
+    for _ in range(3):
+        for key, t in (("without", None), ("with_counts", cnt)):
+            bind(t)
+            step_fn(5)
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            step_fn(50)
+            e1.record()
+            torch.cuda.synchronize()
+            step_ms[key].append(e0.elapsed_time(e1) / 50)
+    # the counts now belong to the last step's adjacency (the last loop ran with them bound)
+    ms1, nnz1 = timed(cnt[:m].reshape(-1))
+    bind(None)
+    read1 = adj_read + B * 8
+    written1 = nnz1 * 20 + (B + 2) * 8
+    out["one_pass"] = {"ms_per_call": ms1, "nnz": nnz1, "algorithmic_bytes": read1 + written1,
+                       "achieved_GBps": (read1 + written1) / (ms1 * 1e-3) / 1e9,
+                       "frac_hbm_peak": (read1 + written1) / (ms1 * 1e-3) / 1e9 / PEAK_HBM_GBPS,
+                       "step_ms_without_counts": step_ms["without"], "step_ms_with_counts": step_ms["with_counts"],
+                       "note": "scan of the step kernel's per-graph counts + emit: the adjacency read once"}
+    return out
 
 
 def cpu_share():
@@ -213,6 +256,16 @@ def synthetic_actions(t, env0, n_envs, N, device):
     return (((x >> 33) & 0x7FFFFFFF) % 25).to(torch.int32)
 
 
+def parse_kernel_select(spec):
+    """--kernel-select "team=2,lanes_per_env=64" -> {"team": 2, ...} (lsm_kernel_select fields, A/B runs
+    only; None = the library's own choice, which every reported line uses)."""
+    out = {}
+    for item in filter(None, (spec or "").split(",")):
+        k, _, v = item.partition("=")
+        out[k.strip()] = int(v)
+    return out or None
+
+
 def timed_window(warmup, steps, epl):
     """Untimed steps before the timed window: at least `warmup`, and as many more as put an
     episode boundary (the auto-reset launch and the episode-summary collective) in the middle of
@@ -268,6 +321,8 @@ def main():
                          "'edges' object to the JSON line (SURVEY 8(f) row 2; not part of the step)")
     ap.add_argument("--rng", default="mt19937", choices=("mt19937", "philox"),
                     help="device reset stream: mt19937 = the reference's draws (default), philox = fast mode")
+    ap.add_argument("--kernel-select", default="",
+                    help="A/B runs only: lsm_kernel_select fields, e.g. team=2 (include/lsm_rollout.h)")
     ap.add_argument("--dry-run", action="store_true",
                     help="no GPU: check the rank launch, env offsets and collectives with gloo")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
@@ -316,7 +371,7 @@ def main():
     layout = c.get("adj_layout", "reference")
     env = GpuGraphVecEnv(args, num_envs=n_envs, device=dev, value_table=vt, ttr_table=tt,
                          env_offset=rank * n_envs, return_numpy=False, build_infos=False, adj_layout=layout,
-                         rng=a.rng)
+                         rng=a.rng, kernel_select=parse_kernel_select(a.kernel_select))
     N = c["num_agents"]
     epl = c["episode_length"]
     pre = timed_window(a.warmup, a.steps, epl)
@@ -361,28 +416,30 @@ def main():
     import gc
     gc.collect()
     gc.disable()
-    for t in range(pre):
-        one_step(t)
-    summaries.results()
+    try:
+        for t in range(pre):
+            one_step(t)
+        summaries.results()
     # Kernel time: HIP events on the launch stream bracketing the whole timed region (per-launch
     # event pairs would add their own GPU-side markers between back-to-back launches). Both are
     # recorded once before the window: the HIP events are created at their first record.
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    ev0.record()
-    ev1.record()
-    torch.cuda.synchronize()
-    barrier(a.dist_backend)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    ev0.record()
-    for t in range(a.steps):
-        one_step(pre + t)
-    ev1.record()
-    torch.cuda.synchronize()
-    barrier(a.dist_backend)
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    gc.enable()
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev0.record()
+        ev1.record()
+        torch.cuda.synchronize()
+        barrier(a.dist_backend)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ev0.record()
+        for t in range(a.steps):
+            one_step(pre + t)
+        ev1.record()
+        torch.cuda.synchronize()
+        barrier(a.dist_backend)
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+    finally:   # an exception in the window must not leave the collector off
+        gc.enable()
     kern_ms = ev0.elapsed_time(ev1) / a.steps   # includes the inter-launch gaps (conservative)
     per_rank = [elapsed * 1e3 / a.steps]
     if world > 1:
@@ -439,7 +496,15 @@ def main():
             "episode_summaries_timed": ep_summaries,
         }
         if a.edges:
-            line["edges"] = bench_edges(env, dev)
+            extra = {"t": pre + a.steps}
+
+            def more_steps(k):
+                for _ in range(k):
+                    t = extra["t"]
+                    env.step_async(synthetic_actions(t, rank * n_envs, n_envs, N, dev), ep)
+                    env.step_wait()
+                    extra["t"] = t + 1
+            line["edges"] = bench_edges(env, dev, more_steps)
         print(json.dumps(line), flush=True)
     env.close()
     if world > 1:

@@ -72,7 +72,11 @@ enum {
                                    lsm_config.collision_forces (core.py:741-774; never applied) */
   LSM_OUT_DEPARTED = 16,  /* uint8   [n][N]   agent.departed after the call (info 'Departed',
                              navigation_graph_safe.py:446); written when bound                 */
-  LSM_NUM_OUT = 17
+  LSM_OUT_ADJ_NNZ = 17,   /* int64  [n][N]    nonzeros of each ego's adjacency as stored (either layout:
+                             the per-graph count of GNNBase.process_adj's adj.nonzero(), gnn.py:376-407),
+                             written when bound; lsm_edges_scan_emit takes it so the edge list needs
+                             one adjacency pass. One-wave and team kernels (E <= 64) only */
+  LSM_NUM_OUT = 18
 };
 
 /* Scenario sources (lsm_config.scenario).
@@ -182,6 +186,30 @@ typedef struct lsm_curriculum {
 
 int lsm_create(const lsm_config* cfg, lsm_env** out);
 void lsm_destroy(lsm_env* env);
+
+/* Kernel selection for parity tests and A/B runs (no reference counterpart: the reference has one
+ * Python implementation). lsm_create picks the kernel from the configuration alone; the library
+ * reads no environment variables. Fields at their "default" value keep lsm_create's choice.
+ *   workgroup_per_env  1: rollout_block_kernel even where a one-wave kernel fits (default 0)
+ *   lanes_per_env      one-wave kernels: 64 (one env per wave, default; 0 = 64), 32 or 16 (2 / 4
+ *                      envs per wave, needs num_agents <= lanes_per_env)
+ *   team               -1 default (4 envs per workgroup for DI N = 8 and airtaxi N = 16), 0 the
+ *                      plain one-wave kernel, 2 / 4 / 8 (team * num_agents <= 64)
+ *   generic            1: never the compile-time-N instantiations (default 0)
+ *   lean               -1 default (airtaxi team kernel: lean LDS layout), 0: the full table
+ *   filter_search      -1 default (1: bound-pruned exact argmin in the workgroup kernel), 0: full search
+ *   bounds_shift       0 default (2): log2 of the cells per dimension of a value-bounds block (1..4) */
+typedef struct lsm_kernel_select {
+  int32_t workgroup_per_env;
+  int32_t lanes_per_env;
+  int32_t team;
+  int32_t generic;
+  int32_t lean;
+  int32_t filter_search;
+  int32_t bounds_shift;
+} lsm_kernel_select;
+/* lsm_create with an explicit kernel selection (sel == NULL: lsm_create's defaults). */
+int lsm_create_select(const lsm_config* cfg, const lsm_kernel_select* sel, lsm_env** out);
 const char* lsm_last_error(const lsm_env* env);
 
 /* values: float32 [prod(shape)] (values_hj, already negated/shifted); grads: float32
@@ -301,6 +329,12 @@ int lsm_host_scenario(const lsm_config* cfg, const lsm_curriculum* cur, uint32_t
  *                    offsets[B]; edge_index holds 2*cap int64 and edge_attr cap floats (cap >= nnz,
  *                    e.g. B*E*E), filled as [2][nnz] / [nnz][1] from their start; nothing is
  *                    written when nnz > cap (the caller checks offsets[B] afterwards)
+ *   lsm_edges_scan_emit  one adjacency pass: `counts` int64 [B] = each graph's nonzeros as the step
+ *                    kernel wrote them (LSM_OUT_ADJ_NNZ of the call that wrote `adj`), so there is
+ *                    no count pass: scan into offsets (int64 [B + 2]: offsets[B] = nnz, offsets[B + 1]
+ *                    = the number of graphs whose nonzeros differed from their count, 0 when the
+ *                    counts belong to `adj`; such a graph's slot is zero-filled) and emit as
+ *                    lsm_edges_emit_dev does (nothing written when nnz > cap)
  * Errors: nonzero return, text in lsm_edges_last_error() (per host thread). */
 size_t lsm_edges_workspace_bytes(int64_t B);
 int lsm_edges_count(const float* adj, const uint64_t* masks, int64_t B, int32_t E, int32_t N,
@@ -311,6 +345,9 @@ int lsm_edges_emit(const float* adj, const uint64_t* masks, int64_t B, int32_t E
 int lsm_edges_emit_dev(const float* adj, const uint64_t* masks, int64_t B, int32_t E, int32_t N,
                        const int64_t* offsets, int64_t cap, int64_t* edge_index, float* edge_attr,
                        void* hip_stream);
+int lsm_edges_scan_emit(const float* adj, const uint64_t* masks, int64_t B, int32_t E, int32_t N,
+                        const int64_t* counts, int64_t* offsets, void* workspace, size_t workspace_bytes,
+                        int64_t cap, int64_t* edge_index, float* edge_attr, void* hip_stream);
 const char* lsm_edges_last_error(void);
 
 /* ---- Buffer insert: the derived rows of GMPERunner.insert / warmup (lsm_buffer.hip) ----------

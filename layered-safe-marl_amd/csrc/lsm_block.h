@@ -203,6 +203,10 @@ void rollout_block_kernel(const KParams* __restrict__ Pp, const KStep K) {
   const int MW = (E + 63) >> 6;
   constexpr int T = NT ? block_tpe(NT) : 64;      // butterfly bound (generic: up to 64 lanes)
   const int TE = NT ? T : block_tpe(N);           // threads per ego actually used
+#ifdef LSM_XP_POISON
+  LDS_POISON(smem, P.lds_env_bytes, tid, BT);
+  __syncthreads();
+#endif
   Lds S = carve_block(smem, N, NL, E, F);
   // RealisticScenario departure arrays (airtaxi layouts; the Bay Area intersection at 16 agents)
   if (DYN == 1 && NT == 0 && P.scenario == LSM_SCENARIO_DEPARTURES) carve_dep(S, smem, P.lds_dep_off, N);

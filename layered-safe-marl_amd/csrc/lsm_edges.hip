@@ -51,18 +51,53 @@ __device__ __forceinline__ int lane_id() { return __lane_id(); }
 // distance of (k + 0.5) / E from an integer is >= 0.5 / E >= 1/512, far above fp32 rounding.
 __device__ __forceinline__ int row_of(int k, float inv_e) { return (int)(((float)k + 0.5f) * inv_e); }
 
-__device__ __forceinline__ bool masked(const uint64_t* m, int r, int c) {
-  return ((m[r >> 6] >> (r & 63)) & 1ull) | ((m[c >> 6] >> (c & 63)) & 1ull);
+// The compact layout's disconnect words of one graph (W = ceil(E / 64) <= 4), loaded once per wave
+// before its element loads and held in registers. Round 5's kernels read the word of every element
+// from global memory next to the element's own load; a 4-chunk variant of them undercounted one
+// edge in a few graphs of some calls on unchanged inputs (profiles/r05_s21_edges_diag.txt). With
+// the words in registers the only global loads left in the element loop are the adjacency values.
+struct MaskRegs {
+  uint64_t w0, w1, w2, w3;
+  bool on;   // compact layout
+};
+
+__device__ __forceinline__ MaskRegs load_masks(const uint64_t* m, int W) {
+  MaskRegs M;
+  M.on = m != nullptr;
+  M.w0 = M.w1 = M.w2 = M.w3 = 0ull;
+  if (M.on) {
+    // wave-uniform address: one load per word for the wave, complete before the first use
+    M.w0 = m[0];
+    if (W > 1) M.w1 = m[1];
+    if (W > 2) M.w2 = m[2];
+    if (W > 3) M.w3 = m[3];
+  }
+  return M;
+}
+
+// bit r of the graph's disconnect words, by selects (no branch on the lane-varying word index)
+__device__ __forceinline__ uint32_t mbit(const MaskRegs& M, int r) {
+  const uint32_t q = (uint32_t)r >> 6;
+  uint64_t x = M.w0;
+  x = q == 1u ? M.w1 : x;
+  x = q == 2u ? M.w2 : x;
+  x = q == 3u ? M.w3 : x;
+  return (uint32_t)(x >> (r & 63)) & 1u;
+}
+
+// v, or +0.0 when row r or column c is disconnected (the reference assigns 0 to those entries,
+// navigation_graph_safe.py:976-989): an AND with an all-ones / all-zeros word, branch-free
+__device__ __forceinline__ float mask_val(float v, const MaskRegs& M, int r, int c) {
+  const uint32_t drop = mbit(M, r) | mbit(M, c);
+  return __uint_as_float(__float_as_uint(v) & (drop - 1u));
 }
 
 // Value of element k of graph b (0 where masked in the compact layout).
-__device__ __forceinline__ float load_val(const AdjSrc& s, int64_t b, const float* g, const uint64_t* m,
-                                          int k) {
+__device__ __forceinline__ float load_val(const AdjSrc& s, const float* g, const MaskRegs& M, int k) {
   const float v = __builtin_nontemporal_load(g + k);
-  if (m == nullptr) return v;
+  if (!M.on) return v;
   const int r = row_of(k, s.inv_e);
-  const int c = k - r * s.E;
-  return masked(m, r, c) ? 0.0f : v;
+  return mask_val(v, M, r, k - r * s.E);
 }
 
 __device__ __forceinline__ const float* graph_ptr(const AdjSrc& s, int64_t b) {
@@ -74,21 +109,21 @@ __device__ __forceinline__ const float* graph_ptr(const AdjSrc& s, int64_t b) {
 // elements with one 16-B load; its nonzero count c in [0, 4] is spread over 3 ballots (bit k of c),
 // so the exclusive prefix over lanes is sum_k 2^k * popcount(ballot_k below the lane).
 template <int VEC>
-__device__ __forceinline__ int lane_vals(const AdjSrc& s, int64_t b, const float* g, const uint64_t* m, int k,
-                                         int EE, float (&v)[VEC]) {
+__device__ __forceinline__ int lane_vals(const AdjSrc& s, const float* g, const MaskRegs& M, int k, int EE,
+                                         float (&v)[VEC]) {
   int c = 0;
   if (VEC == 1) {
-    v[0] = k < EE ? load_val(s, b, g, m, k) : 0.0f;
+    v[0] = k < EE ? load_val(s, g, M, k) : 0.0f;
     c = v[0] != 0.0f;
   } else {
     if (k < EE) {
       const f32x4 q = __builtin_nontemporal_load((const f32x4*)(g + k));
       v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
-      if (m) {
+      if (M.on) {
 #pragma unroll
         for (int i = 0; i < VEC; ++i) {
           const int r = row_of(k + i, s.inv_e);
-          if (masked(m, r, k + i - r * s.E)) v[i] = 0.0f;
+          v[i] = mask_val(v[i], M, r, k + i - r * s.E);
         }
       }
     } else {
@@ -111,12 +146,12 @@ __global__ __launch_bounds__(256) void edge_count_kernel(AdjSrc s, int64_t* __re
   const int64_t b = (int64_t)blockIdx.x * GRAPHS_PER_BLOCK + (threadIdx.x >> 6);
   if (b >= s.B) return;   // whole wave exits together
   const float* g = graph_ptr(s, b);
-  const uint64_t* m = s.masks ? s.masks + b * s.W : nullptr;
+  const MaskRegs M = load_masks(s.masks ? s.masks + b * s.W : nullptr, s.W);
   const int EE = s.E * s.E;
   int cnt = 0;
   for (int k0 = 0; k0 < EE; k0 += WAVE * VEC) {
     float v[VEC];
-    const int c = lane_vals<VEC>(s, b, g, m, k0 + VEC * lane_id(), EE, v);
+    const int c = lane_vals<VEC>(s, g, M, k0 + VEC * lane_id(), EE, v);
     if (VEC == 1) {
       cnt += __popcll(__ballot(c != 0));
     } else {
@@ -133,10 +168,13 @@ __global__ __launch_bounds__(256) void edge_count_kernel(AdjSrc s, int64_t* __re
 // the edge would scatter each instruction over partial lines.
 // nnz < 0: read it on the device (offsets[B]); the outputs then hold `cap` edges, and nothing is
 // written when nnz > cap (the caller sees nnz and reports it).
+// bad != nullptr: the offsets came from counts the caller supplied (the step kernel's
+// LSM_OUT_ADJ_NNZ), not from this file's count pass; a graph whose nonzeros differ from its slot
+// (offsets[b + 1] - offsets[b]) increments *bad, and its slot is zero-filled rather than left unset.
 template <int VEC>
 __global__ __launch_bounds__(256) void edge_emit_kernel(AdjSrc s, const int64_t* __restrict__ offsets,
                                                         int64_t nnz, int64_t cap, int64_t* __restrict__ edge_index,
-                                                        float* __restrict__ edge_attr) {
+                                                        float* __restrict__ edge_attr, int64_t* __restrict__ bad) {
   __shared__ int32_t sk[GRAPHS_PER_BLOCK][WAVE * VEC];
   __shared__ float sv[GRAPHS_PER_BLOCK][WAVE * VEC];
   const int w = threadIdx.x >> 6;
@@ -147,17 +185,22 @@ __global__ __launch_bounds__(256) void edge_emit_kernel(AdjSrc s, const int64_t*
     if (nnz > cap) return;
   }
   const float* g = graph_ptr(s, b);
-  const uint64_t* m = s.masks ? s.masks + b * s.W : nullptr;
+  const MaskRegs M = load_masks(s.masks ? s.masks + b * s.W : nullptr, s.W);
   const int EE = s.E * s.E;
   const int lane = lane_id();
   const int64_t node0 = b * s.E;
-  int64_t pos = offsets[b];
+  const int64_t pos0 = offsets[b];
+  int64_t pos = pos0;
   const int64_t end = offsets[b + 1];
-  if (end > nnz) return;   // caller's nnz is stale: write nothing rather than out of bounds
-  for (int k0 = 0; k0 < EE && pos < end; k0 += WAVE * VEC) {
+  if (end > nnz || pos0 > end) {   // caller's nnz is stale / bad counts: write nothing out of bounds
+    if (bad && lane == 0) atomicAdd((unsigned long long*)bad, 1ull);
+    return;
+  }
+  int64_t found = 0;   // the graph's nonzeros (checked against its slot when the counts are given)
+  for (int k0 = 0; k0 < EE && (bad || pos < end); k0 += WAVE * VEC) {
     const int k = k0 + VEC * lane;
     float v[VEC];
-    const int c = lane_vals<VEC>(s, b, g, m, k, EE, v);
+    const int c = lane_vals<VEC>(s, g, M, k, EE, v);
     uint32_t pre;
     int tot;
     if (VEC == 1) {
@@ -169,6 +212,7 @@ __global__ __launch_bounds__(256) void edge_emit_kernel(AdjSrc s, const int64_t*
       pre = below(b0) + 2 * below(b1) + 4 * below(b2);
       tot = __popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2);
     }
+    found += tot;
     if (c) {
       int o = (int)pre;
 #pragma unroll
@@ -184,7 +228,8 @@ __global__ __launch_bounds__(256) void edge_emit_kernel(AdjSrc s, const int64_t*
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    for (int t = lane; t < tot; t += WAVE) {
+    const int room = (int)(end - pos < (int64_t)tot ? end - pos : (int64_t)tot);   // never past the slot
+    for (int t = lane; t < room; t += WAVE) {
       const int kk = sk[w][t];
       const int r = row_of(kk, s.inv_e);
       edge_index[pos + t] = node0 + r;
@@ -192,7 +237,23 @@ __global__ __launch_bounds__(256) void edge_emit_kernel(AdjSrc s, const int64_t*
       edge_attr[pos + t] = sv[w][t];
     }
     __builtin_amdgcn_wave_barrier();   // slots are rewritten by the next chunk
-    pos += tot;
+    pos += room;
+  }
+  if (bad && found != end - pos0) {
+    for (int64_t t = pos + lane; t < end; t += WAVE) {   // a short graph: its slot's tail zeroed
+      edge_index[t] = 0;
+      edge_index[nnz + t] = 0;
+      edge_attr[t] = 0.0f;
+    }
+    if (lane == 0) atomicAdd((unsigned long long*)bad, 1ull);
+  }
+}
+
+// offsets[0] = 0 and the error word offsets[B + 1] = 0 before the scan / emit of the counts path
+__global__ void offsets_init_kernel(int64_t* offsets, int64_t B) {
+  if (threadIdx.x == 0) {
+    offsets[0] = 0;
+    offsets[B + 1] = 0;
   }
 }
 
@@ -270,10 +331,10 @@ int lsm_edges_emit(const float* adj, const uint64_t* masks, int64_t B, int32_t E
   const int64_t blocks = (B + GRAPHS_PER_BLOCK - 1) / GRAPHS_PER_BLOCK;
   if (E % 2 == 0)
     edge_emit_kernel<4><<<dim3((unsigned)blocks), 256, 0, (hipStream_t)stream>>>(s, offsets, nnz, nnz, edge_index,
-                                                                                 edge_attr);
+                                                                                 edge_attr, nullptr);
   else
     edge_emit_kernel<1><<<dim3((unsigned)blocks), 256, 0, (hipStream_t)stream>>>(s, offsets, nnz, nnz, edge_index,
-                                                                                 edge_attr);
+                                                                                 edge_attr, nullptr);
   return hipGetLastError() == hipSuccess ? 0 : fail("launch failed");
 }
 
@@ -289,10 +350,41 @@ int lsm_edges_emit_dev(const float* adj, const uint64_t* masks, int64_t B, int32
   const int64_t blocks = (B + GRAPHS_PER_BLOCK - 1) / GRAPHS_PER_BLOCK;
   if (E % 2 == 0)
     edge_emit_kernel<4><<<dim3((unsigned)blocks), 256, 0, (hipStream_t)stream>>>(s, offsets, -1, cap, edge_index,
-                                                                                 edge_attr);
+                                                                                 edge_attr, nullptr);
   else
     edge_emit_kernel<1><<<dim3((unsigned)blocks), 256, 0, (hipStream_t)stream>>>(s, offsets, -1, cap, edge_index,
-                                                                                 edge_attr);
+                                                                                 edge_attr, nullptr);
+  return hipGetLastError() == hipSuccess ? 0 : fail("launch failed");
+}
+
+int lsm_edges_scan_emit(const float* adj, const uint64_t* masks, int64_t B, int32_t E, int32_t N,
+                        const int64_t* counts, int64_t* offsets, void* workspace, size_t workspace_bytes, int64_t cap,
+                        int64_t* edge_index, float* edge_attr, void* stream) {
+  AdjSrc s;
+  if (make_src(adj, masks, B, E, N, &s)) return 1;
+  if (B > INT32_MAX) return fail("B exceeds the scan's int32 item count");
+  if (!counts || !offsets) return fail("counts / offsets is null");
+  if (cap < 0) return fail("cap < 0");
+  if (cap > 0 && (!edge_index || !edge_attr)) return fail("edge_index / edge_attr is null");
+  if (workspace_bytes < lsm_edges_workspace_bytes(B)) return fail("workspace too small");
+  hipStream_t st = (hipStream_t)stream;
+  offsets_init_kernel<<<1, 64, 0, st>>>(offsets, B);
+  if (B == 0) return hipGetLastError() == hipSuccess ? 0 : fail("launch failed");
+  const size_t cbytes = ((size_t)B * sizeof(int64_t) + 255) & ~(size_t)255;
+  void* temp = (char*)workspace + cbytes;
+  size_t tbytes = workspace_bytes - cbytes;
+  if (hipcub::DeviceScan::InclusiveSum(temp, tbytes, counts, offsets + 1, (int)B, st) != hipSuccess)
+    return fail("scan failed");
+  if (cap > 0) {
+    const int64_t blocks = (B + GRAPHS_PER_BLOCK - 1) / GRAPHS_PER_BLOCK;
+    // the scan above rewrote offsets[B]; the error word offsets[B + 1] was cleared before it
+    if (E % 2 == 0)
+      edge_emit_kernel<4><<<dim3((unsigned)blocks), 256, 0, st>>>(s, offsets, -1, cap, edge_index, edge_attr,
+                                                                  offsets + B + 1);
+    else
+      edge_emit_kernel<1><<<dim3((unsigned)blocks), 256, 0, st>>>(s, offsets, -1, cap, edge_index, edge_attr,
+                                                                  offsets + B + 1);
+  }
   return hipGetLastError() == hipSuccess ? 0 : fail("launch failed");
 }
 

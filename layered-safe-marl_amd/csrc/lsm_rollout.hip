@@ -44,8 +44,23 @@
 #if !defined(LSM_DIAGNOSTIC_BUILD) &&                                                              \
     (defined(LSM_STAMPS) || defined(LSM_XP_VALHOT) || defined(LSM_XP_GRADHOT) || defined(LSM_XP_NOFILT) || \
      defined(LSM_XP_NOOUT) || defined(LSM_XP_NORESETEMIT) || defined(LSM_XP_NORK) || defined(LSM_XP_NOSCEN) || \
-     defined(LSM_XP_DELAY))
+     defined(LSM_XP_DELAY) || defined(LSM_XP_POISON))
 #error "diagnostic switch in a product build: use lsm.build.build_variants (LSM_DIAGNOSTIC_BUILD)"
+#endif
+
+// Diagnostic builds: LSM_XP_POISON=pattern sets every 32-bit word of a workgroup's dynamic LDS to the
+// pattern before the kernel's first LDS access. LDS is not cleared between workgroups, so a read of a
+// word the kernel never wrote returns whatever the CU's previous workgroup left there; under the poison
+// it returns the pattern instead. Outputs that stay equal to the oracle under two different patterns
+// (tests run with LSM_LIB = the poisoned library) do not depend on unwritten LDS.
+#ifdef LSM_XP_POISON
+#define LDS_POISON(base, bytes, tid, nthr)                                                         \
+  do {                                                                                             \
+    for (uint32_t q_ = (uint32_t)(tid); q_ < (uint32_t)(bytes) / 4u; q_ += (uint32_t)(nthr))       \
+      ((uint32_t*)(base))[q_] = (uint32_t)(LSM_XP_POISON);                                         \
+  } while (0)
+#else
+#define LDS_POISON(base, bytes, tid, nthr) do { } while (0)
 #endif
 
 // LSM_PART (lsm.build): 0 = host code only, g > 0 = kernel group g only, undefined = everything
@@ -171,6 +186,7 @@ struct OutDev {
   float* active_masks; // LSM_OUT_ACTIVE_MASKS (optional)
   double* cforce;      // LSM_OUT_COLLISION_FORCE (lsm_config.collision_forces only)
   uint8_t* departed;   // LSM_OUT_DEPARTED (optional)
+  int64_t* adjnnz;     // LSM_OUT_ADJ_NNZ (optional): nonzeros of each ego's adjacency as stored
 };
 
 struct KParams {
@@ -1353,6 +1369,19 @@ __device__ __forceinline__ void filter_prep_oct(const KParams& P, Lds& S, GAS un
     jv = tv ? ojv : jv;
     in = tv ? oin : in;
   }
+  // every lane of the ego holds the same choice: the butterfly is order-independent for the values
+  // it can meet (vpair is never NaN -- a NaN interpolation is stored as +inf, the reference's
+  // np.isnan -> inf -- and ties go to the lower index as np.argmin's first occurrence); only NaN
+  // positions could make lanes disagree, so lane 8 e's result is broadcast to its ego's lanes and
+  // the slot words (written one per lane) always come from one choice
+  {
+    const int src = lane & ~7;
+    d = __shfl(d, src);
+    jd = __shfl(jd, src);
+    v = __shfl(v, src);
+    jv = __shfl(jv, src);
+    in = __shfl((int)in, src) != 0;
+  }
 #ifdef LSM_STAMPS
   if (lane == 0 && stp) stp[32] = __builtin_amdgcn_s_memtime();
 #endif
@@ -1767,6 +1796,33 @@ __device__ __forceinline__ void emit_adj_uniform(const KParams& P, const Lds& S,
 template <int DYN, int LPE, int NT>
 __device__ __forceinline__ void emit_nodes(const KParams& P, Lds& S, int env, bool uni);
 
+// LSM_OUT_ADJ_NNZ: the nonzeros of each ego's adjacency as emit_graph stores it (either layout: the
+// thresholded table with ego e's disconnected rows and columns zeroed) -- the per-graph count of
+// GNNBase.process_adj's adj.nonzero() (gnn.py:376-407), so the learner's edge list takes one pass
+// over the adjacency (lsm_edges_scan_emit) instead of a count pass and an emit pass. Row r's nonzero
+// columns as a ballot word (E <= 64), then lane e adds popcount(word & ~mask_e) over its unmasked
+// rows. The test is on the stored float32 value, exactly what nonzero() sees.
+template <int LPE, int NT>
+__device__ __forceinline__ void emit_adj_nnz(const KParams& P, const Lds& S, int env) {
+  const int lane = threadIdx.x & (LPE - 1);
+  const int gsh = ((int)threadIdx.x & 63) & ~(LPE - 1);   // this env's first lane in the wave
+  constexpr int DYN = 0;
+  LSM_DIMS;
+  const uint64_t me = lane < N ? S.emask[lane] : 0ull;
+  int64_t cnt = 0;
+  for (int r = 0; r < E; ++r) {
+    uint64_t row = 0ull;
+    for (int c0 = 0; c0 < E; c0 += LPE) {
+      const int c = c0 + lane;
+      const uint64_t b = __ballot(c < E && fv1(S, N, NL, E, r, c < E ? c : 0) != 0.0f);
+      const uint64_t gb = LPE == 64 ? b : (b >> gsh) & ((1ull << LPE) - 1ull);
+      row |= gb << c0;
+    }
+    if (lane < N && !((me >> r) & 1ull)) cnt += __popcll(row & ~me);
+  }
+  if (lane < N) gptr(P.o.adjnnz)[(size_t)env * N + lane] = cnt;
+}
+
 // `adj_done`: the uniform adjacency was already stored (speculatively, in phase D of the team
 // kernel); it is rewritten here only if an agent changed status.
 template <int DYN, int LPE, int NT>
@@ -1843,6 +1899,7 @@ __device__ __forceinline__ void emit_graph(const KParams& P, Lds& S, int env, bo
     }
   }
   emit_nodes<DYN, LPE, NT>(P, S, env, uni);
+  if (gptr(P.o.adjnnz)) emit_adj_nnz<LPE, NT>(P, S, env);
 }
 
 // node_obs [N][E][F] of one env (DI rows / airtaxi trig table already in LDS). `uni`: no
@@ -3162,6 +3219,10 @@ __global__ __launch_bounds__(64, DYN == 0 ? (LPE == 64 ? 4 : 2) : LSM_WAVES_PER_
   if (env >= P.n_envs) return;
   LSM_DIMS;
   unsigned char* lbase = smem + (size_t)grp * P.lds_env_bytes;
+#ifdef LSM_XP_POISON
+  LDS_POISON(lbase, P.lds_env_bytes, lane, LPE);
+  __syncthreads();
+#endif
   Lds S = carve(lbase, N, NL, E, F);
   // RealisticScenario departures run only here: the generic airtaxi kernel, one env per wave
   if (DYN == 1 && NT == 0 && LPE == 64 && P.scenario == LSM_SCENARIO_DEPARTURES) carve_dep(S, lbase, P.lds_dep_off, N);
@@ -3443,9 +3504,10 @@ struct lsm_env {
   int32_t ring_cap;    // KParams copies allocated in dring
   int32_t ring_sel;    // -1: plain bindings
   KParams* dring;
-  int lpe;   // lanes per env
-  bool block;   // workgroup-per-env kernel (N > 32 or E > 64, or LSM_KERNEL=block)
-  bool generic_only;   // LSM_GENERIC=1: never use the compile-time-N kernels (tests): 64 (one env per wave), 32 or 16 (2 or 4 envs per wave)
+  lsm_kernel_select sel;   // lsm_create_select's kernel choice (tests, A/B runs)
+  int lpe;   // lanes per env: 64 (one env per wave), 32 or 16 (2 or 4 envs per wave)
+  bool block;   // workgroup-per-env kernel (N > 32 or E > 64, or sel.workgroup_per_env)
+  bool generic_only;   // sel.generic: never use the compile-time-N kernels (tests)
   int team;   // envs per workgroup of the team kernel (lsm_team.h); 0 = rollout_kernel
   bool lean;  // the team kernel's lean LDS layout (airtaxi, N % 4 == 0, E % 4 == 0)
 };
@@ -3568,8 +3630,7 @@ static void fill_params(const lsm_env* e, KParams& P) {
   P.use_filter_arg = e->cfg.use_safety_filter;
   P.auto_reset = e->cfg.auto_reset;
   P.adj_compact = e->cfg.adj_layout == LSM_ADJ_COMPACT;
-  P.filter_search = 1;
-  if (const char* v = getenv("LSM_FILTER_SEARCH")) P.filter_search = atoi(v);
+  P.filter_search = e->sel.filter_search == 0 ? 0 : 1;
   P.scenario = e->cfg.scenario;
   P.rng = e->cfg.rng;
   P.nis = e->cfg.num_internal_step > 1 ? e->cfg.num_internal_step : 1;
@@ -3649,6 +3710,7 @@ static void fill_params(const lsm_env* e, KParams& P) {
   P.o.active_masks = (float*)e->out_ptr[LSM_OUT_ACTIVE_MASKS];
   P.o.cforce = e->cfg.collision_forces ? (double*)e->out_ptr[LSM_OUT_COLLISION_FORCE] : nullptr;
   P.o.departed = (uint8_t*)e->out_ptr[LSM_OUT_DEPARTED];
+  P.o.adjnnz = (int64_t*)e->out_ptr[LSM_OUT_ADJ_NNZ];
   P.stamps = (unsigned long long*)e->out_ptr[LSM_OUT_DEBUG_STAMPS];
   P.diag = 0;
 #ifdef LSM_STAMPS
@@ -3680,6 +3742,7 @@ size_t lsm_output_bytes(const lsm_env* e, int32_t slot) {
     case LSM_OUT_ACTIVE_MASKS: return n * N * 4;
     case LSM_OUT_COLLISION_FORCE: return n * N * 2 * 8;
     case LSM_OUT_DEPARTED: return n * N;
+    case LSM_OUT_ADJ_NNZ: return n * N * 8;
     default: return 0;
   }
 }
@@ -3692,12 +3755,34 @@ int32_t lsm_node_features(const lsm_env* e) { return e->F; }
 int32_t lsm_obs_dim(const lsm_env* e) { return e->OBS; }
 const char* lsm_last_error(const lsm_env* e) { return e ? e->err.c_str() : "null handle"; }
 
-int lsm_create(const lsm_config* cfg, lsm_env** out) {
+int lsm_create(const lsm_config* cfg, lsm_env** out) { return lsm_create_select(cfg, nullptr, out); }
+
+int lsm_create_select(const lsm_config* cfg, const lsm_kernel_select* sel, lsm_env** out) {
   *out = nullptr;
   if (!cfg) return 1;
   lsm_env* e = new lsm_env();
   *out = e;
   e->cfg = *cfg;
+  if (sel) {
+    e->sel = *sel;
+  } else {
+    memset(&e->sel, 0, sizeof(e->sel));
+    e->sel.team = -1;
+    e->sel.lean = -1;
+    e->sel.filter_search = -1;
+  }
+  {
+    const lsm_kernel_select& s = e->sel;
+    if (s.workgroup_per_env != 0 && s.workgroup_per_env != 1) return fail(e, "kernel select: workgroup_per_env must be 0 or 1");
+    if (s.generic != 0 && s.generic != 1) return fail(e, "kernel select: generic must be 0 or 1");
+    if (s.lanes_per_env != 0 && s.lanes_per_env != 16 && s.lanes_per_env != 32 && s.lanes_per_env != 64)
+      return fail(e, "kernel select: lanes_per_env must be 0, 16, 32 or 64");
+    if (s.team != -1 && s.team != 0 && s.team != 2 && s.team != 4 && s.team != 8)
+      return fail(e, "kernel select: team must be -1, 0, 2, 4 or 8");
+    if (s.lean < -1 || s.lean > 1) return fail(e, "kernel select: lean must be -1, 0 or 1");
+    if (s.filter_search < -1 || s.filter_search > 1) return fail(e, "kernel select: filter_search must be -1, 0 or 1");
+    if (s.bounds_shift < 0 || s.bounds_shift > 4) return fail(e, "kernel select: bounds_shift must be in [0, 4]");
+  }
   e->tables_ok = false;
   e->dparams = nullptr;
   for (int k = 0; k < LSM_NUM_OUT; ++k) {
@@ -3734,10 +3819,7 @@ int lsm_create(const lsm_config* cfg, lsm_env** out) {
   if (cfg->scenario == LSM_SCENARIO_DEPARTURES && cfg->dynamics != LSM_AIRTAXI)
     return fail(e, "departure timers need airtaxi dynamics (RealisticScenario calls "
                    "reset_velocity(theta, speed), KinematicVehicleXYState only, core.py:137)");
-  {
-    const char* kv = getenv("LSM_KERNEL");
-    e->block = N > MAXN || N * (1 + L) > MAXE || (kv && strcmp(kv, "block") == 0);
-  }
+  e->block = N > MAXN || N * (1 + L) > MAXE || e->sel.workgroup_per_env == 1;
   if (cfg->num_envs < 1) return fail(e, "num_envs must be >= 1");
   if (cfg->num_internal_step < 0 || cfg->num_internal_step > 64)
     return fail(e, "num_internal_step must be in [0, 64] (0 and 1: one inner step)");
@@ -3751,37 +3833,34 @@ int lsm_create(const lsm_config* cfg, lsm_env** out) {
   e->OBS = cfg->dynamics == LSM_DOUBLE_INTEGRATOR ? 7 : 6;
   // Lanes per env: 64 = one env per wave (default; measured fastest at 4096 envs, where
   // 4 waves/SIMD hide LDS/HBM latency), 32/16 = 2/4 envs per wave sharing the per-agent
-  // instruction stream (needs N <= lanes). LSM_LPE overrides.
-  e->lpe = 64;
-  if (const char* v = getenv("LSM_LPE")) e->lpe = atoi(v);
-  e->generic_only = getenv("LSM_GENERIC") && atoi(getenv("LSM_GENERIC")) != 0;
-  if (e->block) e->lpe = 64;   // LSM_LPE applies to the one-wave kernel only
+  // instruction stream (needs N <= lanes). sel.lanes_per_env overrides.
+  e->lpe = e->sel.lanes_per_env ? e->sel.lanes_per_env : 64;
+  e->generic_only = e->sel.generic == 1;
+  if (e->block) e->lpe = 64;   // lanes_per_env applies to the one-wave kernel only
   if (cfg->scenario != LSM_SCENARIO_TRAIN) {   // layouts: the generic one-wave kernel (mode 2 resets)
     e->generic_only = true;
     e->lpe = 64;
   }
   // Team kernel (lsm_team.h) for the compile-time-N BASELINE agent counts: G envs per
-  // workgroup share one wave for their per-agent phases. LSM_TEAM=0 selects rollout_kernel,
-  // LSM_TEAM=G another instantiated G.
+  // workgroup share one wave for their per-agent phases. sel.team = 0 selects rollout_kernel,
+  // sel.team = G another instantiated G.
   e->team = 0;
   // the team kernel runs World.step's inner loop once (num_internal_step = 1, the training
   // default, train.sh:35); more inner steps run in rollout_kernel / the workgroup kernel
   if (!e->block && e->lpe == 64 && L == 2 && !e->generic_only && cfg->num_internal_step <= 1) {
     if (cfg->dynamics == LSM_DOUBLE_INTEGRATOR && N == 8) e->team = 4;   // measured: 4 < 8 < 2 (us/step)
     if (cfg->dynamics == LSM_AIRTAXI && N == 16) e->team = 4;   // lean LDS: 4 < 2 < 0 (us/step)
-    if (const char* v = getenv("LSM_TEAM")) {
-      const int g = atoi(v);
-      if (g == 0) e->team = 0;
-      else if (e->team && g * N <= 64 && (g == 2 || g == 4 || g == 8)) e->team = g;
-      else if (e->team) return fail(e, "LSM_TEAM must be 0, 2, 4 or 8 with LSM_TEAM * num_agents <= 64");
-    }
+    const int g = e->sel.team;
+    if (g == 0) e->team = 0;
+    else if (g > 0 && e->team && g * N <= 64) e->team = g;
+    else if (g > 0 && e->team) return fail(e, "kernel select: team * num_agents must be <= 64");
   }
   // lean LDS layout for the airtaxi team kernel (6 -> 8 envs per CU at N = 16);
-  // LSM_LEAN=0 keeps the full table (A/B)
+  // sel.lean = 0 keeps the full table (A/B)
   e->lean = e->team && cfg->dynamics == LSM_AIRTAXI && (N & 3) == 0 && (e->E & 3) == 0;
-  if (const char* v = getenv("LSM_LEAN")) e->lean = e->lean && atoi(v) != 0;
+  if (e->sel.lean == 0) e->lean = false;
   if (!(e->lpe == 16 || e->lpe == 32 || e->lpe == 64) || e->lpe < (e->block ? 1 : N))
-    return fail(e, "LSM_LPE must be 16, 32 or 64 and >= num_agents");
+    return fail(e, "kernel select: lanes_per_env must be 16, 32 or 64 and >= num_agents");
   HIPCHK(e, hipGetDevice(&e->device));
   const size_t n = cfg->num_envs;
   int r = 0;
@@ -3958,8 +4037,8 @@ static int upload_table(lsm_env* e, TableDev& T, int32_t ndim, const double* lo,
 
 // Value bounds per 4^ndim-cell block (TableDev::bnd), built from the node table.
 static int upload_bounds(lsm_env* e, TableDev& T, const float* values) {
-  T.bshift = 2;   // 4 cells per dim: 180 KB for the full DI table (L2-resident)
-  if (const char* v = getenv("LSM_BOUNDS_SHIFT")) T.bshift = atoi(v);
+  // 4 cells per dim: 180 KB for the full DI table (L2-resident); sel.bounds_shift for tests
+  T.bshift = e->sel.bounds_shift ? e->sel.bounds_shift : 2;
   const int B = 1 << T.bshift;
   int nblocks = 1;
   for (int d = T.ndim - 1; d >= 0; --d) {
@@ -4030,7 +4109,7 @@ int lsm_bind_output_ring(lsm_env* e, int32_t slot, void* base, size_t stride_byt
   if (!e) return 1;
   if (slot < 0 || slot >= LSM_NUM_OUT) return fail(e, "bad output slot");
   if (slot == LSM_OUT_RESET_FLAG || slot == LSM_OUT_EP_INFO || slot == LSM_OUT_EDGES ||
-      slot == LSM_OUT_DEBUG_STAMPS || slot == LSM_OUT_DEPARTED)
+      slot == LSM_OUT_DEBUG_STAMPS || slot == LSM_OUT_DEPARTED || slot == LSM_OUT_ADJ_NNZ)
     return fail(e, "slot " + std::to_string(slot) + " cannot be ring-bound");
   if (count <= 0 || !base) {   // unbind
     e->ring_count[slot] = 0;
@@ -4069,6 +4148,9 @@ static int check_ready(lsm_env* e, bool stepping) {
     return fail(e, "compact adjacency layout needs LSM_OUT_ADJ_MASK bound");
   if (e->cfg.collision_forces && !e->out_ptr[LSM_OUT_COLLISION_FORCE])
     return fail(e, "collision_forces needs LSM_OUT_COLLISION_FORCE bound");
+  if (e->block && e->out_ptr[LSM_OUT_ADJ_NNZ])
+    return fail(e, "LSM_OUT_ADJ_NNZ is written by the one-wave and team kernels (E <= 64); the workgroup-per-env "
+                   "kernel's edge lists take lsm_edges_count's pass");
   (void)stepping;
   return 0;
 }

@@ -416,6 +416,10 @@ void rollout_team_kernel(const KParams* __restrict__ Pp, const KStep K) {
   LSM_DIMS;
   const uint32_t B = P.lds_env_bytes;
   unsigned char* lbase = smem + (size_t)w * B;
+#ifdef LSM_XP_POISON
+  LDS_POISON(lbase, B, lane, 64);
+  __syncthreads();
+#endif
   Lds S = carve(lbase, N, NL, E, F, DYN == 1 && P.lean != 0);   // folds away for the DI kernels
   // agent view: lane = g * NT + i
   const int ag = lane / NT;

@@ -17,8 +17,8 @@ LSM_DOUBLE_INTEGRATOR, LSM_AIRTAXI = 0, 1
 LSM_ACTIONS_INDEX_I32, LSM_ACTIONS_ONEHOT_F32, LSM_ACTIONS_ONEHOT_F64 = 0, 1, 2
 (OUT_OBS, OUT_NODE_OBS, OUT_ADJ, OUT_REWARD, OUT_DONE, OUT_RESET_FLAG, OUT_EP_INFO, OUT_INFO,
  OUT_EDGES, OUT_STATE, OUT_DEBUG_STAMPS, OUT_ADJ_MASK, OUT_SHARE_OBS, OUT_MASKS, OUT_ACTIVE_MASKS,
- OUT_COLLISION_FORCE, OUT_DEPARTED) = range(17)
-NUM_OUT = 17
+ OUT_COLLISION_FORCE, OUT_DEPARTED, OUT_ADJ_NNZ) = range(18)
+NUM_OUT = 18
 LSM_SCENARIO_TRAIN, LSM_SCENARIO_LAYOUT, LSM_SCENARIO_DEPARTURES = 0, 1, 2
 LSM_RNG_MT19937, LSM_RNG_PHILOX = 0, 1
 ADJ_REFERENCE, ADJ_COMPACT = 0, 1
@@ -37,7 +37,8 @@ EXPORTED = ("lsm_create", "lsm_destroy", "lsm_last_error", "lsm_set_value_table"
             "lsm_edges_last_error", "lsm_bind_output_ring", "lsm_select_ring", "lsm_buffer_insert",
             "lsm_buffer_last_error", "lsm_host_rk45_di", "lsm_host_glibc_pow", "lsm_action_errors",
             "lsm_kernel_name", "lsm_reset_layout", "lsm_layout_doubles", "lsm_host_philox_uniforms",
-            "lsm_host_philox4x32", "lsm_episode_summary", "lsm_build_id", "lsm_test_set_mt_stage")
+            "lsm_host_philox4x32", "lsm_episode_summary", "lsm_build_id", "lsm_test_set_mt_stage",
+            "lsm_create_select", "lsm_edges_scan_emit")
 
 
 class LsmConfig(C.Structure):
@@ -48,6 +49,24 @@ class LsmConfig(C.Structure):
                 ("world_size", C.c_double), ("seed", C.c_int64), ("env_offset", C.c_int64),
                 ("collision_forces", C.c_int32), ("scenario", C.c_int32), ("rng", C.c_int32),
                 ("num_internal_step", C.c_int32), ("reward_terms", C.c_int32), ("collaborative", C.c_int32)]
+
+
+class LsmKernelSelect(C.Structure):
+    """lsm_kernel_select: kernel choice for parity tests and A/B runs (the library reads no
+    environment variables). ``kernel_select(**overrides)`` fills the defaults."""
+    _fields_ = [(n, C.c_int32) for n in ("workgroup_per_env", "lanes_per_env", "team", "generic", "lean",
+                                         "filter_search", "bounds_shift")]
+
+
+KERNEL_SELECT_DEFAULTS = dict(workgroup_per_env=0, lanes_per_env=0, team=-1, generic=0, lean=-1, filter_search=-1,
+                              bounds_shift=0)
+
+
+def kernel_select(**overrides) -> LsmKernelSelect:
+    bad = set(overrides) - set(KERNEL_SELECT_DEFAULTS)
+    if bad:
+        raise ValueError("unknown kernel_select fields: %s" % sorted(bad))
+    return LsmKernelSelect(**dict(KERNEL_SELECT_DEFAULTS, **overrides))
 
 
 class LsmCurriculum(C.Structure):
@@ -76,6 +95,7 @@ def load_library(path: str = LIB_PATH):
     P, I32, I64, U32, D, SZ = C.c_void_p, C.c_int32, C.c_int64, C.c_uint32, C.c_double, C.c_size_t
     sig = {
         "lsm_create": (I32, [C.POINTER(LsmConfig), C.POINTER(P)]),
+        "lsm_create_select": (I32, [C.POINTER(LsmConfig), C.POINTER(LsmKernelSelect), C.POINTER(P)]),
         "lsm_destroy": (None, [P]),
         "lsm_last_error": (C.c_char_p, [P]),
         "lsm_set_value_table": (I32, [P, I32, P, P, P, P, P, P, D]),
@@ -94,6 +114,7 @@ def load_library(path: str = LIB_PATH):
         "lsm_edges_count": (I32, [P, P, I64, I32, I32, P, P, SZ, P]),
         "lsm_edges_emit": (I32, [P, P, I64, I32, I32, P, I64, P, P, P]),
         "lsm_edges_emit_dev": (I32, [P, P, I64, I32, I32, P, I64, P, P, P]),
+        "lsm_edges_scan_emit": (I32, [P, P, I64, I32, I32, P, P, P, SZ, I64, P, P, P]),
         "lsm_edges_last_error": (C.c_char_p, []),
         "lsm_bind_output_ring": (I32, [P, I32, P, SZ, I32, I32]),
         "lsm_select_ring": (I32, [P, I32]),

@@ -32,6 +32,8 @@ def main():
     ap.add_argument("--envs", type=int, default=0)
     ap.add_argument("--team", action="store_true",
                     help="the team kernel's stamps (lsm_team.h): phases A-E, work vs barrier wait")
+    ap.add_argument("--kernel-select", default="",
+                    help="lsm_kernel_select fields, e.g. team=2 (include/lsm_rollout.h; default: the library's choice)")
     ap.add_argument("--pick", default="",
                     help="comma-separated step indices to keep (e.g. 250: the step after the first "
                          "episode boundary at episode length 250); default every step from 10 on")
@@ -53,8 +55,11 @@ def main():
     vt, tt = hj_tables.default_tables(c["dynamics_type"]) if (c["use_safety_filter"] or
                                                               c["dynamics_type"] != "double_integrator") else (None, None)
     n_envs = a.envs or c["envs"]
+    ksel = bench.parse_kernel_select(a.kernel_select)
     env = GpuGraphVecEnv(args, num_envs=n_envs, device="cuda:0", value_table=vt, ttr_table=tt,
-                         return_numpy=False, build_infos=False, adj_layout=c.get("adj_layout", "reference"))
+                         return_numpy=False, build_infos=False, adj_layout=c.get("adj_layout", "reference"),
+                         kernel_select=ksel)
+    G = ksel.get("team", 4) if ksel and ksel.get("team", -1) > 0 else 4
     stamps = torch.zeros((n_envs, 40), dtype=torch.int64, device="cuda:0")   # LSM_NSTAMP
     capi.check(env.lib.lsm_bind_output(env.h, capi.OUT_DEBUG_STAMPS, C.c_void_p(stamps.data_ptr()),
                                        stamps.numel() * 8), env.h)
@@ -91,7 +96,6 @@ def main():
                                                       np.percentile(v, 90)))
         print("%-18s %12.0f" % ("total", tot))
         # per wave slot (env % G): phase medians and end time; and the slowest 2 % of waves
-        G = int(os.environ.get("LSM_TEAM", "4"))
         slots = np.concatenate([np.arange(x.shape[0]) % G for x in tstamps])
         rts = np.concatenate([x[:, 1] for x in rt])   # end (ns since the launch's first wave start)
         print("slot   " + " ".join("%10s" % n[:10] for n, _, _ in segs) + "      end us")
@@ -151,7 +155,6 @@ def main():
     if a.team:
         # SIMD placement of each wave slot w of the team workgroups (env = G * block + w), and how
         # many distinct SIMDs the agent-phase waves (w = 0 for B, w = 1 for D) of one CU occupy
-        G = int(os.environ.get("LSM_TEAM", "4"))
         slot = np.arange(len(simd)) % G
         cukey = xcc * np.uint64(1000) + se * np.uint64(100) + cu
         for w in range(G):

@@ -97,14 +97,19 @@ def expand_compact_adj(adj, mask, E):
 
 class GpuGraphVecEnv(ShareVecEnv):
     """rng: "mt19937" (the reference's draws, default) or "philox" (fast device resets, same
-    scenario distribution). layout: an evaluation ScenarioLayout (needs auto_reset=False)."""
+    scenario distribution). layout: an evaluation ScenarioLayout (needs auto_reset=False).
+    kernel_select: tests / A/B runs only, fields of lsm_kernel_select (include/lsm_rollout.h), e.g.
+    {"workgroup_per_env": 1} or {"team": 0}; None = the library's own choice.
+    emit_edge_counts: the step also writes each ego graph's adjacency nonzeros (LSM_OUT_ADJ_NNZ, E <= 64
+    kernels), and edge_list() builds the learner's edge list in one pass over the adjacency."""
 
     def __init__(self, all_args, num_envs: Optional[int] = None, device=None,
                  value_table: Optional[HjTable] = None, ttr_table: Optional[HjTable] = None,
                  auto_reset: bool = True, env_offset: int = 0, emit_edges: bool = False,
                  return_numpy: bool = True, build_infos: bool = True, small_tables: bool = False,
                  adj_layout: str = "reference", collision_forces: bool = False,
-                 layout: Optional[ScenarioLayout] = None, rng: str = "mt19937"):
+                 layout: Optional[ScenarioLayout] = None, rng: str = "mt19937",
+                 kernel_select: Optional[dict] = None, emit_edge_counts: bool = False):
         torch = _torch()
         self.args = EnvArgs.from_namespace(all_args) if not isinstance(all_args, EnvArgs) else all_args
         self.args.validate()
@@ -157,7 +162,10 @@ class GpuGraphVecEnv(ShareVecEnv):
         if int(a.seed) + 1000 * (int(env_offset) + self.num_envs - 1) >= 2 ** 32:
             raise ValueError("numpy seeds must be < 2**32 (seed + 1000 * env index)")
         h = C.c_void_p()
-        rc = self.lib.lsm_create(C.byref(cfg), C.byref(h))
+        if kernel_select:   # tests / A/B runs: an explicit kernel (capi.KERNEL_SELECT_DEFAULTS)
+            rc = self.lib.lsm_create_select(C.byref(cfg), C.byref(capi.kernel_select(**kernel_select)), C.byref(h))
+        else:
+            rc = self.lib.lsm_create(C.byref(cfg), C.byref(h))
         self.h = h
         capi.check(rc, h)
         # HJ / TTR tables (synthetic stand-ins for the absent pickles unless given); the HJ handle exists
@@ -195,6 +203,8 @@ class GpuGraphVecEnv(ShareVecEnv):
         self.t_info = torch.zeros((n, N, len(capi.INFO_FIELDS)), dtype=torch.float64, device=dev)
         self.t_state = torch.zeros((n, N, 4), dtype=torch.float64, device=dev)
         self.t_edges = torch.zeros((n, E, E), dtype=torch.uint8, device=dev) if emit_edges else None
+        # per-ego adjacency nonzeros (LSM_OUT_ADJ_NNZ): edge_list() then reads the adjacency once
+        self.t_adj_nnz = torch.zeros((n, N), dtype=torch.int64, device=dev) if emit_edge_counts else None
         # World.get_entity_collision_force per agent (optional report; never applied, like the reference)
         self.t_cforce = torch.zeros((n, N, 2), dtype=torch.float64, device=dev) if collision_forces else None
         # info 'Departed' (RealisticScenario departure timers)
@@ -206,7 +216,7 @@ class GpuGraphVecEnv(ShareVecEnv):
                         (capi.OUT_EP_INFO, self.t_epinfo), (capi.OUT_INFO, self.t_info),
                         (capi.OUT_STATE, self.t_state), (capi.OUT_EDGES, self.t_edges),
                         (capi.OUT_ADJ_MASK, self.t_adj_mask), (capi.OUT_COLLISION_FORCE, self.t_cforce),
-                        (capi.OUT_DEPARTED, self.t_departed)):
+                        (capi.OUT_DEPARTED, self.t_departed), (capi.OUT_ADJ_NNZ, self.t_adj_nnz)):
             if t is None:
                 continue
             capi.check(self.lib.lsm_bind_output(h, slot, C.c_void_p(t.data_ptr()),
@@ -379,8 +389,8 @@ class GpuGraphVecEnv(ShareVecEnv):
         edge_attr float32 [nnz, 1]), built on the GPU from either adjacency layout."""
         from . import edges
         if self.t_adj_mask is None:
-            return edges.process_adj(self.t_adj.view(-1, self.E, self.E))
-        return edges.process_adj_compact(self.t_adj, self.t_adj_mask, self.N)
+            return edges.process_adj(self.t_adj.view(-1, self.E, self.E), counts=self.t_adj_nnz)
+        return edges.process_adj_compact(self.t_adj, self.t_adj_mask, self.N, counts=self.t_adj_nnz)
 
     def set_agent_state(self, env_index: int, agent_state, reached=None):
         """Overwrite one env's agent states ([N][4]) and optionally reached_goal ([N])."""

@@ -3,10 +3,10 @@ only compared within one run). Each variant = a library (LSM_LIB, see lsm.build 
 environment settings; the variants are run round-robin `--reps` times.
 
     python layered-safe-marl_amd/tools/ab_bench.py --config 3 --reps 2 \\
-        base: team4:LSM_TEAM=4 nosplit:LSM_TEAM=4,LSM_LIB=liblsm_rollout_nosplit.so
+        base: team2:KSEL=team=2 nosplit:LSM_LIB=liblsm_rollout_nosplit.so
 
-A variant is NAME:K=V,K=V (LSM_LIB relative to csrc/). Prints one line per variant: the median
-ms per step and each run's.
+A variant is NAME:K=V,K=V (LSM_LIB relative to csrc/; KSEL=field=value;field=value passes
+bench.py --kernel-select). Prints one line per variant: the median ms per step and each run's.
 """
 from __future__ import annotations
 
@@ -28,7 +28,8 @@ def parse(v):
     for item in filter(None, kv.split(",")):
         k, _, val = item.partition("=")
         env[k] = os.path.join(CSRC, val) if k == "LSM_LIB" else val
-    return name, env
+    ksel = env.pop("KSEL", "").replace(";", ",")
+    return name, env, ksel
 
 
 def main():
@@ -43,14 +44,16 @@ def main():
     ap.add_argument("--bench-args", default="", help="extra bench.py arguments (e.g. '--steps 20')")
     a = ap.parse_args()
     vs = [parse(v) for v in a.variants]
-    res = {n: [] for n, _ in vs}
+    res = {n: [] for n, _, _ in vs}
     for _ in range(a.reps):
-        for name, extra in vs:
+        for name, extra, ksel in vs:
             env = dict(os.environ, **extra)
             if a.allow_old:
                 env["LSM_LIB_AB"] = "1"
             cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--config", str(a.config), "--steps",
                    str(a.steps), "--warmup", str(a.warmup), "--no-cpu-baseline"] + a.bench_args.split()
+            if ksel:
+                cmd += ["--kernel-select", ksel]
             out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
             if out.returncode != 0:
                 print(name, "FAILED", out.stderr[-2000:], flush=True)
@@ -59,7 +62,7 @@ def main():
             res[name].append(d["ms_per_step"] * 1e3)
             print("%-12s %8.2f us  (%s)" % (name, res[name][-1], d["roofline"]["kernel"]), flush=True)
     print("---- config %d, median us/step over %d reps" % (a.config, a.reps))
-    for name, _ in vs:
+    for name, _, _ in vs:
         print("%-12s %8.2f   %s" % (name, statistics.median(res[name]), " ".join("%.2f" % x for x in res[name])))
 
 

@@ -183,3 +183,28 @@ def test_host_scenario_philox_distribution(lib, dyn, n):
     d = np.array(seen)
     # the separation draw retries up to 1000 times: essentially every pair satisfies it
     assert np.mean((d > dmin) & (d < dmax)) > 0.95
+
+
+def test_product_source_reads_no_environment_knobs():
+    """Kernel choice is lsm_create_select's explicit lsm_kernel_select (tests, A/B runs), never an
+    environment variable: every getenv in the rollout sources sits inside a diagnostic-build block
+    (LSM_STAMPS / LSM_DIAGNOSTIC_BUILD, which product builds refuse)."""
+    import os
+    import re
+    csrc = os.path.join(os.path.dirname(__file__), "..", "layered-safe-marl_amd", "csrc")
+    for name in sorted(os.listdir(csrc)):
+        if not name.endswith((".hip", ".h")):
+            continue
+        stack = []
+        for ln, line in enumerate(open(os.path.join(csrc, name)), 1):
+            t = line.strip()
+            if re.match(r"#\s*if", t):
+                stack.append(t)
+            elif re.match(r"#\s*endif", t):
+                stack.pop()
+            elif re.match(r"#\s*else", t) and stack:
+                stack[-1] = "else of " + stack[-1]
+            if "getenv(" in line and not t.startswith("//"):
+                guards = [g for g in stack if not g.startswith("else of") and
+                          ("LSM_STAMPS" in g or "LSM_DIAGNOSTIC_BUILD" in g)]
+                assert guards, "%s:%d reads the environment outside a diagnostic block" % (name, ln)

@@ -225,7 +225,7 @@ def test_gpu_edges_emit_dev_writes_nothing_past_cap():
     a = _gpu(_random_adj(rng, 16, 24, density=0.8))
     B, E = 16, 24
     st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
-    off = torch.empty(B + 1, dtype=torch.int64, device="cuda:0")
+    off = torch.empty(B + 2, dtype=torch.int64, device="cuda:0")
     wsb = int(lib.lsm_edges_workspace_bytes(B))
     ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device="cuda:0")
     assert lib.lsm_edges_count(C.c_void_p(a.data_ptr()), None, B, E, 1, C.c_void_p(off.data_ptr()),
@@ -238,6 +238,107 @@ def test_gpu_edges_emit_dev_writes_nothing_past_cap():
                                   C.c_void_p(ei.data_ptr()), C.c_void_p(ea.data_ptr()), st) == 0
     torch.cuda.synchronize()
     assert bool((ei == -7).all()) and bool((ea == -7.0).all())
+
+
+@pytest.mark.gpu
+def test_gpu_bounded_result_storage_is_o_nnz():
+    """a bounded-path result must not pin the B*E*E*20-byte buffers when it holds far
+    fewer edges -- it is copied to exact size (storage <= SHRINK_RATIO x the exact bytes)."""
+    from lsm import edges
+    rng = np.random.default_rng(17)
+    B, E = 2000, 24
+    a = _random_adj(rng, B, E, density=0.02, specials=False)
+    want = ora_process_adj(a)
+    ei, ea = edges.process_adj(_gpu(a))
+    _assert_same((ei.cpu().numpy(), ea.cpu().numpy()), want)
+    nnz = want[0].shape[1]
+    assert nnz * edges.SHRINK_RATIO < B * E * E
+    assert ei.untyped_storage().nbytes() <= edges.SHRINK_RATIO * 16 * nnz
+    assert ea.untyped_storage().nbytes() <= edges.SHRINK_RATIO * 4 * nnz
+
+
+@pytest.mark.gpu
+def test_gpu_process_adj_compact_repeatable_config3():
+    """Round 5's intermittent undercount (profiles/r05_s21_edges_diag.txt: a variant reading the mask
+    word of every element from global memory lost one edge in a few graphs of some calls): the
+    shipped count, on a config-3 compact adjacency with disconnect bits, 24 times on unchanged
+    inputs, every per-graph count equal to numpy's."""
+    import torch
+    from lsm import hj_tables
+    from lsm.config import EnvArgs
+    from lsm.vec_env import GpuGraphVecEnv
+    args = EnvArgs(num_agents=8, num_env_steps=250 * 4, use_safety_filter=True, seed=0)
+    vt, _ = hj_tables.default_tables("double_integrator", small=True)
+    env = GpuGraphVecEnv(args, num_envs=4096, device="cuda:0", value_table=vt, return_numpy=False,
+                         build_infos=False, adj_layout="compact")
+    env.reset(4)
+    g = torch.Generator(device="cuda:0").manual_seed(3)
+    for _ in range(40):   # agents reach goals: disconnect bits set in many graphs
+        env.step(torch.randint(0, 25, (4096, 8), generator=g, device="cuda:0", dtype=torch.int32), 4)
+    assert int((env.t_adj_mask != 0).sum()) > 0
+    want = (env.reference_adj().reshape(-1, env.E, env.E) != 0).sum(dim=(1, 2)).cpu().numpy()
+    from lsm import capi, edges
+    import ctypes as C
+    lib = capi.load_library()
+    B = 4096 * 8
+    st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    off = torch.empty(B + 2, dtype=torch.int64, device="cuda:0")
+    wsb = int(lib.lsm_edges_workspace_bytes(B))
+    ws = torch.empty(wsb, dtype=torch.uint8, device="cuda:0")
+    for rep in range(24):
+        assert lib.lsm_edges_count(C.c_void_p(env.t_adj.data_ptr()), C.c_void_p(env.t_adj_mask.data_ptr()), B,
+                                   env.E, 8, C.c_void_p(off.data_ptr()), C.c_void_p(ws.data_ptr()), wsb, st) == 0
+        got = np.diff(off[:B + 1].cpu().numpy())
+        np.testing.assert_array_equal(got, want, err_msg="call %d" % rep)
+    env.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["di8_team", "di8_team_compact", "di8_wave", "di3_lpe16", "di5_lpe32",
+                                  "at16_team_lean", "at4_generic"])
+def test_gpu_step_edge_counts_one_pass(case):
+    """LSM_OUT_ADJ_NNZ: the step kernel's per-ego nonzero counts equal the stored adjacency's (numpy
+    count of the reference-layout adj, either output layout, across auto-resets and goal / done
+    status changes), and edge_list()'s one-pass path (lsm_edges_scan_emit) equals the oracle's
+    process_adj bit for bit; counts of another adjacency are refused."""
+    import torch
+    from lsm import edges, hj_tables
+    from lsm.config import EnvArgs
+    from lsm.vec_env import GpuGraphVecEnv
+    spec = dict(di8_team=("double_integrator", 8, "reference", None),
+                di8_team_compact=("double_integrator", 8, "compact", None),
+                di8_wave=("double_integrator", 8, "reference", {"team": 0}),
+                di3_lpe16=("double_integrator", 3, "reference", {"lanes_per_env": 16}),
+                di5_lpe32=("double_integrator", 5, "reference", {"lanes_per_env": 32}),
+                at16_team_lean=("airtaxi", 16, "reference", None),
+                at4_generic=("airtaxi", 4, "compact", {"generic": 1}))[case]
+    dyn, N, layout, ksel = spec
+    ws = 4 if dyn == "double_integrator" else 6
+    args = EnvArgs(dynamics_type=dyn, num_agents=N, world_size=ws, episode_length=12, num_env_steps=12 * 4,
+                   use_safety_filter=True, seed=4)
+    n = 37
+    env = GpuGraphVecEnv(args, num_envs=n, device="cuda:0", small_tables=True, return_numpy=False,
+                         build_infos=False, adj_layout=layout, kernel_select=ksel, emit_edge_counts=True)
+    if ksel is None:
+        assert env.kernel_name.startswith("rollout_team_kernel<")
+    env.reset(4)
+    E = env.E
+    rng = np.random.default_rng(N)
+    for t in range(30):   # resets at steps 11 and 23
+        env.step(rng.integers(0, 25, (n, N)), 4)
+        ref = env.reference_adj().reshape(-1, E, E)
+        want = (ref != 0).sum(dim=(1, 2)).cpu().numpy()
+        np.testing.assert_array_equal(env.t_adj_nnz.reshape(-1).cpu().numpy(), want, err_msg="step %d" % t)
+        ei, ea = env.edge_list()
+        _assert_same((ei.cpu().numpy(), ea.cpu().numpy()), ora_process_adj(ref.cpu().numpy()))
+    bad = env.t_adj_nnz.clone()
+    bad[3, 1] += 1
+    with pytest.raises(edges.EdgeError, match="differ"):
+        if layout == "compact":
+            edges.process_adj_compact(env.t_adj, env.t_adj_mask, N, counts=bad)
+        else:
+            edges.process_adj(env.t_adj.view(-1, E, E), counts=bad)
+    env.close()
 
 
 def test_scratch_reuse_keys_and_bound():
@@ -258,9 +359,9 @@ def test_scratch_reuse_keys_and_bound():
     o1, w1, n1 = edges._scratch(lib, dev, 0, 10)
     o2, w2, n2 = edges._scratch(lib, dev, 0, 10)
     assert o1 is o2 and w1 is w2 and n1 == n2 == 64 * 10 + 256 and _Lib.calls == 1
-    assert o1.shape == (11,) and o1.dtype == torch.int64 and w1.numel() == n1
+    assert o1.shape == (12,) and o1.dtype == torch.int64 and w1.numel() == n1   # [B + 2]: + error word
     assert edges._scratch(lib, dev, 1, 10)[0] is not o1      # another stream: its own buffers
-    assert edges._scratch(lib, dev, 0, 11)[0].shape == (12,)  # another graph count
+    assert edges._scratch(lib, dev, 0, 11)[0].shape == (13,)  # another graph count
     for b in range(20, 40):
         edges._scratch(lib, dev, 0, b)
     assert len(edges._SCRATCH) <= 8

@@ -31,26 +31,24 @@ def _info_col(name):
     return capi.INFO_FIELDS.index(name)
 
 
-def _gpu_layout_env(meta, n_envs=1, seed=None):
+def _gpu_layout_env(meta, n_envs=1, seed=None, kernel_select=None):
     from lsm.config import EnvArgs
     from lsm.vec_env import GpuGraphVecEnv
     args = EnvArgs.from_namespace(type("A", (), meta)())
     args.seed = meta["env_seed"] if seed is None else seed
     vt, tt = tables_for(meta)
     return GpuGraphVecEnv(args, num_envs=n_envs, device="cuda:0", value_table=vt, ttr_table=tt,
-                          auto_reset=False, emit_edges=True)
+                          auto_reset=False, emit_edges=True, kernel_select=kernel_select)
 
 
 @pytest.mark.parametrize("kernel", ["auto", "block"])
 @pytest.mark.parametrize("name", layout_fixture_names())
-def test_gpu_layout_matches_reference(name, kernel, monkeypatch):
+def test_gpu_layout_matches_reference(name, kernel):
     """Every layout fixture through the default dispatch (the one-wave generic kernel for
     E <= 64; the workgroup kernel for the Bay Area intersection at 16 agents, E = 112) and through
-    the workgroup kernel forced (LSM_KERNEL=block)."""
-    if kernel == "block":
-        monkeypatch.setenv("LSM_KERNEL", "block")
+    the workgroup kernel forced (kernel_select workgroup_per_env)."""
     z, meta = load(name)
-    env = _gpu_layout_env(meta)
+    env = _gpu_layout_env(meta, kernel_select={"workgroup_per_env": 1} if kernel == "block" else None)
     N = meta["num_agents"]
     big = N * (1 + env.layout.L) > 64
     assert env.kernel_name.startswith("rollout_block_kernel<" if (big or kernel == "block") else "rollout_kernel<")
@@ -178,21 +176,19 @@ def test_gpu_layout_rejects_training_calls():
 
 @pytest.mark.parametrize("dyn,n,kernel", [("double_integrator", 8, "team"), ("double_integrator", 8, "block"),
                                           ("airtaxi", 16, "team"), ("double_integrator", 5, "wave")])
-def test_gpu_philox_reset(dyn, n, kernel, monkeypatch):
+def test_gpu_philox_reset(dyn, n, kernel):
     """LSM_RNG_PHILOX: reset 0 of env k equals lsm_host_scenario(Philox, key seed + 1000 k); across
     auto-resets every scenario stays in the reference's boxes and differs from the previous one."""
     import ctypes as C
     from lsm import capi, curriculum
     from lsm.config import EnvArgs
     from lsm.vec_env import GpuGraphVecEnv
-    if kernel == "block":
-        monkeypatch.setenv("LSM_KERNEL", "block")
     ws = 4 if dyn == "double_integrator" else 6
     args = EnvArgs(dynamics_type=dyn, num_agents=n, world_size=ws, episode_length=12, num_env_steps=12 * 4,
                    use_safety_filter=True, seed=9)
     nenv = 64
     env = GpuGraphVecEnv(args, num_envs=nenv, device="cuda:0", rng="philox", small_tables=True,
-                         return_numpy=False)
+                         return_numpy=False, kernel_select={"workgroup_per_env": 1} if kernel == "block" else None)
     env.reset(4)
     st0 = env.state().cpu().numpy().copy()
     lib = capi.load_library()

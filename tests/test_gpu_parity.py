@@ -32,13 +32,13 @@ GPU_FIXTURES = list(fixture_names())
 
 @pytest.mark.parametrize("kernel", ["wave", "block", "blockc"])
 @pytest.mark.parametrize("name", GPU_FIXTURES)
-def test_gpu_matches_reference_golden(name, kernel, monkeypatch):
+def test_gpu_matches_reference_golden(name, kernel):
     """Every golden fixture through the one-wave kernel and the workgroup-per-env kernel
-    (LSM_KERNEL=block; "blockc": compact adjacency layout, expanded for the comparison)."""
-    if kernel != "wave":
-        monkeypatch.setenv("LSM_KERNEL", "block")
+    (kernel_select workgroup_per_env; "blockc": compact adjacency layout, expanded for the comparison)."""
+    ksel = {"workgroup_per_env": 1} if kernel != "wave" else None
     z, meta = load(name)
-    env = _gpu_env(meta, emit_edges=True, adj_layout="compact" if kernel == "blockc" else "reference")
+    env = _gpu_env(meta, emit_edges=True, adj_layout="compact" if kernel == "blockc" else "reference",
+                   kernel_select=ksel)
     obs, aid, node, adj, ep = env.reset(meta["ep"])
     np.testing.assert_allclose(obs[0], z["reset0_obs"], rtol=0, atol=F32_ATOL)
     np.testing.assert_allclose(node[0], z["reset0_node"], rtol=0, atol=F32_ATOL)
@@ -179,12 +179,12 @@ def _oracle_run(case):
 
 @pytest.mark.parametrize("lpe", [16, 32, 64, "64w", "t2", "t4", "t8", "64g", "block", "blockc"])
 @pytest.mark.parametrize("case", range(len(CASES)))
-def test_gpu_matches_oracle_multi_env(case, lpe, monkeypatch):
+def test_gpu_matches_oracle_multi_env(case, lpe):
     """16 (or 15: a partly filled last wave / workgroup) envs with per-env seeds seed + 1000 k,
     random actions, across an auto-reset; every kernel variant: 1, 2 or 4 envs/wave; at one env
     per wave the default dispatch ("64": the team kernel for N = 8 double integrator (8 envs per
     workgroup) and N = 16 airtaxi (4 per workgroup), the compile-time-N rollout_kernel for
-    N = 3), the one-wave rollout_kernel forced ("64w", LSM_TEAM=0), the team kernel with 2 / 4
+    N = 3), the one-wave rollout_kernel forced ("64w", team 0), the team kernel with 2 / 4
     envs per workgroup ("t2", "t4", "t8"; one fewer env than a whole number of workgroups), the
     generic kernel ("64g"), and the workgroup-per-env
     kernel in both adjacency layouts ("block", "blockc"). The oracle's trajectory is computed once
@@ -199,22 +199,23 @@ def test_gpu_matches_oracle_multi_env(case, lpe, monkeypatch):
         pytest.skip("8 airtaxi envs of 16 agents do not fit one 64-lane agent wave")
     # "t4" at airtaxi N = 16: 4 envs x 19.3 KB in the lean LDS layout (77 KB per workgroup)
     partial = lpe in (16, 32, "t2", "t4", "t8")
+    ksel = {}
     if lpe in ("t2", "t4", "t8", "64w"):
-        monkeypatch.setenv("LSM_TEAM", "0" if lpe == "64w" else lpe[1:])
+        ksel["team"] = 0 if lpe == "64w" else int(lpe[1:])
         lpe = 64
     layout = "reference"
     if lpe in ("block", "blockc"):
-        monkeypatch.setenv("LSM_KERNEL", "block")
+        ksel["workgroup_per_env"] = 1
         layout = "compact" if lpe == "blockc" else "reference"
         lpe = 64
     if lpe == "64g":
-        monkeypatch.setenv("LSM_GENERIC", "1")
+        ksel["generic"] = 1
         lpe = 64
-    monkeypatch.setenv("LSM_LPE", str(lpe))
+    ksel["lanes_per_env"] = lpe
     meta, ep, nb = _case_meta(case)
     run = _oracle_run(case)
     n = nb - 1 if partial else nb
-    env = _gpu_env(meta, n_envs=n, seed=5, adj_layout=layout)
+    env = _gpu_env(meta, n_envs=n, seed=5, adj_layout=layout, kernel_select=ksel)
     g = env.reset(ep)
     o = run["reset"]
     np.testing.assert_allclose(g[0], o[0][:n], rtol=0, atol=F32_ATOL)
@@ -247,28 +248,68 @@ def test_gpu_matches_oracle_multi_env(case, lpe, monkeypatch):
     env.close()
 
 
+def _full_tables(meta):
+    """The full-shape synthetic tables bench.py times (lsm.hj_tables.default_tables): DI (61, 61, 41,
+    41), airtaxi (41, 41, 36, 9, 9) + TTR (41, 41, 36, 9) -- not golden_replay.tables_for's small ones."""
+    from lsm import hj_tables
+    return hj_tables.default_tables(meta["dynamics_type"])
+
+
+def _full_env_and_oracles(meta, n_envs, sample, **kw):
+    from lsm.config import EnvArgs
+    from lsm.vec_env import GpuGraphVecEnv
+    from oracle.lsm_oracle import OracleVecEnv
+    args = EnvArgs.from_namespace(type("A", (), meta)())
+    args.seed = meta["env_seed"]
+    vt, tt = _full_tables(meta)
+    env = GpuGraphVecEnv(args, num_envs=n_envs, device="cuda:0", value_table=vt, ttr_table=tt,
+                         return_numpy=False, **kw)
+    oras = [OracleVecEnv(meta, 1, seed=meta["env_seed"], value_table=table_dict(vt), ttr_table=table_dict(tt),
+                         integrator="restated", seed_offset=k) for k in sample]
+    return env, oras
+
+
+def _check_all_envs(ora_all, s, obs, adj, dones, rew, st, ctx):
+    """Step s of every env against the oracle pool's run: dones and adjacency bits exact, obs and
+    rewards within the fp32 tolerance, states within STATE_ATOL."""
+    n = obs.shape[0]
+    np.testing.assert_array_equal(dones.cpu().numpy(), ora_all["dones"][:, s], err_msg=ctx + " dones")
+    bits = np.packbits((adj != 0).reshape(n, -1).cpu().numpy(), axis=1)
+    bad = np.nonzero((bits != ora_all["adj"][:, s]).any(axis=1))[0]
+    assert len(bad) == 0, "%s: adjacency bits differ in envs %s" % (ctx, bad[:10].tolist())
+    np.testing.assert_allclose(obs.cpu().numpy(), ora_all["obs"][:, s], rtol=0, atol=F32_ATOL, err_msg=ctx)
+    np.testing.assert_allclose(rew.cpu().numpy(), ora_all["rew"][:, s], rtol=1e-6, atol=1e-5, err_msg=ctx)
+    np.testing.assert_allclose(st.cpu().numpy(), ora_all["state"][:, s], rtol=0, atol=STATE_ATOL, err_msg=ctx)
+
+
 def test_gpu_full_size_properties_and_sampled_oracle():
-    """BASELINE config 3 size (8 agents x 4096 envs, filter on): invariants over 260 steps
-    (one auto-reset at step 250) + exact replay of sampled envs through the oracle."""
+    """BASELINE config 3 exactly as bench.py times it (8 agents x 4096 envs, filter on, the full-shape
+    (61, 61, 41, 41) HJ table): ALL 4096 envs against the oracle at the reset and the first 3 steps
+    (dones, adjacency bits, obs, rewards, states; the oracle over worker processes, tests/oracle_pool.py);
+    invariants over 260 steps (one auto-reset at step 250) + exact replay of sampled envs through it."""
     import torch
+    from oracle_pool import run_all_envs
     meta = dict(dynamics_type="double_integrator", num_agents=8, num_landmarks=2, world_size=4,
                 episode_length=250, num_env_steps=250 * 4, n_rollout_threads=1, use_safety_filter=True,
                 use_masking=True, num_internal_step=1, seed=0, env_seed=0)
-    n_envs = 4096
-    env = _gpu_env(meta, n_envs=n_envs, seed=0, return_numpy=False)
+    n_envs, N, S_ALL, T = 4096, 8, 3, 260
+    acts = np.random.default_rng(0).integers(0, 25, (T, n_envs, N)).astype(np.int32)
+    ora_all = run_all_envs(meta, 0, n_envs, 4, np.ascontiguousarray(acts[:S_ALL].transpose(1, 0, 2)))
     sample = [0, 1, 1337, 4095]
-    oras = [_oracle_for(meta, 0, 1, env_offset=k) for k in sample]
+    env, oras = _full_env_and_oracles(meta, n_envs, sample)
+    assert env.value_table.shape == (61, 61, 41, 41)
     obs, aid, node, adj, ep = env.reset(4)
+    np.testing.assert_allclose(obs.cpu().numpy(), ora_all["reset_obs"], rtol=0, atol=F32_ATOL)
+    bits = np.packbits((adj != 0).reshape(n_envs, -1).cpu().numpy(), axis=1)
+    np.testing.assert_array_equal(bits, ora_all["reset_adj"])
     for k, o in zip(sample, oras):
-        r = o.reset(4)
-        np.testing.assert_allclose(obs[k].cpu().numpy(), r[0][0], rtol=0, atol=F32_ATOL)
-    gen = torch.Generator(device="cuda:0").manual_seed(0)
-    N = 8
-    for t in range(260):
-        a = torch.randint(0, 25, (n_envs, N), device="cuda:0", generator=gen, dtype=torch.int32)
+        o.reset(4)
+    for t in range(T):
+        a = torch.as_tensor(acts[t], device="cuda:0")
         obs, aid, node, adj, rew, dones, (info, reset, epinfo) = env.step(a, 4)
-        a_h = a.cpu().numpy()
         st = env.state()
+        if t < S_ALL:
+            _check_all_envs(ora_all, t, obs, adj, dones, rew, st, "all envs, step %d" % t)
         if t % 20 == 0 or t >= 248:
             assert torch.isfinite(obs).all() and torch.isfinite(node).all() and torch.isfinite(adj).all()
             assert (adj >= 0).all() and (adj <= 4).all()   # the float32 cast of d < 4 may be 4.0f
@@ -282,7 +323,7 @@ def test_gpu_full_size_properties_and_sampled_oracle():
         elif t < 249:
             assert not bool(reset.any()) or bool(dones.all(dim=1)[reset.bool()].all())
         for k, o in zip(sample, oras):
-            r = o.step(a_h[k:k + 1], 4)
+            r = o.step(acts[t][k:k + 1], 4)
             np.testing.assert_array_equal(dones[k].cpu().numpy(), r[5][0], err_msg="env %d step %d" % (k, t))
             np.testing.assert_array_equal((adj[k] != 0).cpu().numpy(), r[3][0] != 0)
             np.testing.assert_allclose(obs[k].cpu().numpy(), r[0][0], rtol=0, atol=F32_ATOL)
@@ -477,20 +518,19 @@ def _arrive_all(e):
 
 
 @pytest.mark.parametrize("kernel", ["wave", "block"])
-def test_gpu_runner_call_pattern_separation_curriculum(kernel, monkeypatch):
+def test_gpu_runner_call_pattern_separation_curriculum(kernel):
     """GMPERunner's real call pattern (graph_mpe_runner.py:72-103): step(actions, episode) with the
     episode index advancing every episode_length steps, the worker auto-resetting with it
     (env_wrappers.py:866-871). With SEPARATION_DISTANCE_CURRICULUM each reset shifts that env's own
     HJ table (safety_filter.py:170-174 via navigation_graph_safe.py:349-364); envs driven all-done
     mid-episode reset at the newer stair level while the others keep the older one, so envs hold
     different tables at once. 16 envs vs the oracle, every step."""
-    if kernel == "block":
-        monkeypatch.setenv("LSM_KERNEL", "block")
+    ksel = {"workgroup_per_env": 1} if kernel == "block" else None
     epl, ep0, n_envs, N = 60, 3, 16, 3
     meta = dict(dynamics_type="double_integrator", num_agents=N, num_landmarks=2, world_size=4,
                 episode_length=epl, num_env_steps=epl * 10, n_rollout_threads=1, use_safety_filter=True,
                 use_masking=True, num_internal_step=1, seed=9, env_seed=9, separation_distance_curriculum=True)
-    env = _gpu_env(meta, n_envs=n_envs, seed=9)
+    env = _gpu_env(meta, n_envs=n_envs, seed=9, kernel_select=ksel)
     ora = _oracle_for(meta, 9, n_envs)
     g, o = env.reset(ep0), ora.reset(ep0)
     np.testing.assert_allclose(g[0], o[0], rtol=0, atol=F32_ATOL)
@@ -536,19 +576,18 @@ def test_gpu_runner_call_pattern_separation_curriculum(kernel, monkeypatch):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("kernel", ["wave", "block", "team"])
-def test_gpu_separation_chain_unbounded(kernel, monkeypatch):
+def test_gpu_separation_chain_unbounded(kernel):
     """HjDataHandle.update_separation_distance (safety_filter.py:170-174) has no limit: 24 separation
     changes (alternating stair levels, well past the record's 8 slots: the chain continues in the
     per-env HBM overflow, grown twice) and the filter after each still matches the oracle, whose
     table is shifted in place as the reference's is; a re-upload then starts every chain afresh.
     "team": 8 agents, the config-3 kernel (rollout_team_kernel<0, 8, 4>)."""
-    if kernel == "block":
-        monkeypatch.setenv("LSM_KERNEL", "block")
+    ksel = {"workgroup_per_env": 1} if kernel == "block" else None
     meta = dict(dynamics_type="double_integrator", num_agents=8 if kernel == "team" else 4, num_landmarks=2, world_size=4,
                 episode_length=5, num_env_steps=5 * 20, n_rollout_threads=1, use_safety_filter=True,
                 use_masking=True, num_internal_step=1, seed=1, env_seed=1, separation_distance_curriculum=True)
     n = 3
-    env = _gpu_env(meta, n_envs=n, seed=1)
+    env = _gpu_env(meta, n_envs=n, seed=1, kernel_select=ksel)
     ora = _oracle_for(meta, 1, n)
     # stair levels of ep = 0, 4, 8, 12, 16 (0, .25, .5, .75, 1); up and down, 24 changes
     seq = [0] + [4, 8, 12, 16, 12, 8, 4, 8] * 3
@@ -577,28 +616,36 @@ def test_gpu_separation_chain_unbounded(kernel, monkeypatch):
 
 
 def test_gpu_config4_full_size_properties_and_sampled_oracle():
-    """BASELINE config 4 (16 airtaxi agents x 8192 envs, HJ filter on, episode_length 350):
-    rollout_kernel<1, 64, 16> over 360 steps spanning the auto-reset at step 350: invariants
+    """BASELINE config 4 exactly as bench.py times it (16 airtaxi agents x 8192 envs, HJ filter on,
+    episode_length 350, the full-shape (41, 41, 36, 9, 9) value and (41, 41, 36, 9) TTR tables):
+    ALL 8192 envs against the oracle at the reset and the first step (tests/oracle_pool.py);
+    rollout_team_kernel<1, 16, 4> over 360 steps spanning the auto-reset at step 350: invariants
     every 20 steps and around the reset, and sampled envs replayed exactly through the oracle."""
     import torch
+    from oracle_pool import run_all_envs
     meta = dict(dynamics_type="airtaxi", num_agents=16, num_landmarks=2, world_size=6,
                 episode_length=350, num_env_steps=350 * 4, n_rollout_threads=1, use_safety_filter=True,
                 use_masking=True, num_internal_step=1, seed=0, env_seed=0)
-    n_envs, N, E = 8192, 16, 48
-    env = _gpu_env(meta, n_envs=n_envs, seed=0, return_numpy=False)
+    n_envs, N, E, S_ALL, T = 8192, 16, 48, 1, 360
+    acts = np.random.default_rng(4).integers(0, 25, (T, n_envs, N)).astype(np.int32)
+    ora_all = run_all_envs(meta, 0, n_envs, 4, np.ascontiguousarray(acts[:S_ALL].transpose(1, 0, 2)))
     sample = [0, 8191]   # the oracle takes ~36 ms per env-step here
-    oras = [_oracle_for(meta, 0, 1, env_offset=k) for k in sample]
+    env, oras = _full_env_and_oracles(meta, n_envs, sample)
+    assert env.value_table.shape == (41, 41, 36, 9, 9) and env.ttr_table.shape == (41, 41, 36, 9)
     obs, aid, node, adj, ep = env.reset(4)
     assert node.shape == (n_envs, N, E, 11) and adj.shape == (n_envs, N, E, E)
+    np.testing.assert_allclose(obs.cpu().numpy(), ora_all["reset_obs"], rtol=0, atol=F32_ATOL)
+    bits = np.packbits((adj != 0).reshape(n_envs, -1).cpu().numpy(), axis=1)
+    np.testing.assert_array_equal(bits, ora_all["reset_adj"])
     for k, o in zip(sample, oras):
-        r = o.reset(4)
-        np.testing.assert_allclose(obs[k].cpu().numpy(), r[0][0], rtol=0, atol=F32_ATOL)
-    gen = torch.Generator(device="cuda:0").manual_seed(4)
+        o.reset(4)
     vmin, vmax = 60 * 0.514444 * 0.001, 175 * 0.514444 * 0.001
-    for t in range(360):
-        a = torch.randint(0, 25, (n_envs, N), device="cuda:0", generator=gen, dtype=torch.int32)
+    for t in range(T):
+        a = torch.as_tensor(acts[t], device="cuda:0")
         obs, aid, node, adj, rew, dones, (info, reset, epinfo) = env.step(a, 4)
         st = env.state()
+        if t < S_ALL:
+            _check_all_envs(ora_all, t, obs, adj, dones, rew, st, "all envs, step %d" % t)
         if t % 20 == 0 or t >= 348:
             assert torch.isfinite(obs).all() and torch.isfinite(node).all() and torch.isfinite(adj).all()
             assert (adj >= 0).all() and (adj <= 3 * 1.60934 + 1e-6).all()
@@ -610,9 +657,8 @@ def test_gpu_config4_full_size_properties_and_sampled_oracle():
             assert (rew >= -40).all() and (rew <= 50).all()
         if t == 349:
             assert bool(reset.all())
-        a_h = a.cpu().numpy()
         for k, o in zip(sample, oras):
-            r = o.step(a_h[k:k + 1], 4)
+            r = o.step(acts[t][k:k + 1], 4)
             ctx = "env %d step %d" % (k, t)
             np.testing.assert_array_equal(dones[k].cpu().numpy(), r[5][0], err_msg=ctx)
             np.testing.assert_array_equal((adj[k] != 0).cpu().numpy(), r[3][0] != 0, err_msg=ctx)
@@ -648,20 +694,19 @@ def test_gpu_action_index_out_of_range_is_reported():
 
 
 @pytest.mark.parametrize("kernel", ["wave", "block"])
-def test_gpu_collision_forces_reported_never_applied(kernel, monkeypatch):
+def test_gpu_collision_forces_reported_never_applied(kernel):
     """World.get_entity_collision_force (core.py:741-774) has no caller, so the step
     must never apply contact forces. With lsm_config.collision_forces the kernel reports the
     per-agent force (LSM_OUT_COLLISION_FORCE) -- compared with the oracle's restatement (itself
     pinned to the reference's own function, tests/test_collision_forces.py) -- while every output
     stays bit-identical to a run without the flag (the default)."""
-    if kernel == "block":
-        monkeypatch.setenv("LSM_KERNEL", "block")
+    ksel = {"workgroup_per_env": 1} if kernel == "block" else None
     meta = dict(dynamics_type="double_integrator", num_agents=8, num_landmarks=2, world_size=4,
                 episode_length=30, num_env_steps=30 * 4, n_rollout_threads=1, use_safety_filter=True,
                 use_masking=True, num_internal_step=1, seed=13, env_seed=13, collision_forces=True)
     n = 12
-    on = _gpu_env(meta, n_envs=n, seed=13, collision_forces=True)
-    off = _gpu_env(meta, n_envs=n, seed=13)
+    on = _gpu_env(meta, n_envs=n, seed=13, collision_forces=True, kernel_select=ksel)
+    off = _gpu_env(meta, n_envs=n, seed=13, kernel_select=ksel)
     assert off.t_cforce is None
     ora = _oracle_for(meta, 13, n)
     for e in (on, off, ora):
@@ -696,7 +741,7 @@ def test_gpu_collision_forces_reported_never_applied(kernel, monkeypatch):
 
 @pytest.mark.parametrize("team", ["4", "2", "8", "4s"])
 @pytest.mark.parametrize("dyn,N", [("double_integrator", 8), ("airtaxi", 16)])
-def test_gpu_team_kernel_resets_match_oracle(dyn, N, team, monkeypatch):
+def test_gpu_team_kernel_resets_match_oracle(dyn, N, team):
     """The team kernel's auto-resets (all of a workgroup's envs, or some, reset in one launch; each
     resetting env's wave draws its scenario with the agents in parallel from the staged MT19937
     stream, crossing block boundaries over successive resets) against the oracle: 10-step episodes,
@@ -710,13 +755,12 @@ def test_gpu_team_kernel_resets_match_oracle(dyn, N, team, monkeypatch):
     if team == "4s":
         stage = 40
         team = "4"
-    monkeypatch.setenv("LSM_TEAM", team)
     ws = 4 if dyn == "double_integrator" else 6
     meta = dict(dynamics_type=dyn, num_agents=N, num_landmarks=2, world_size=ws, episode_length=10,
                 num_env_steps=10 * 4, n_rollout_threads=1, use_safety_filter=True, use_masking=True,
                 num_internal_step=1, seed=21, env_seed=21)
     n_envs = 15   # a partly filled last workgroup
-    env = _gpu_env(meta, n_envs=n_envs, seed=21)
+    env = _gpu_env(meta, n_envs=n_envs, seed=21, kernel_select={"team": int(team)})
     if stage is not None:
         assert env.lib.lsm_test_set_mt_stage(env.h, stage) == 0
     assert env.kernel_name.startswith("rollout_team_kernel<")
