@@ -115,14 +115,15 @@ def load_traffic(config, n_envs, build_id):
 
 
 def bench_edges(env, dev, step_fn, reps=50):
-    """process_adj (gnn.py:376-407) over this GPU's n*N per-ego graphs, two ways:
-    "count_pass": count kernel + hipcub scan + emit kernel on the last adjacency (the adjacency read
-    twice: the emit pass re-reads it from beyond L2, profiles/r05_s42_edges_traffic.txt);
-    "one_pass": the step kernel also writes each graph's nonzeros (LSM_OUT_ADJ_NNZ), and the call is
-    scan + emit (lsm_edges_scan_emit), the adjacency read once. step_fn(k) runs k more env steps; the
-    step time with and without the counts bound is measured alternately (what the counts cost the step).
-    Algorithmic bytes: adjacency reads (+ mask words, compact) + counts / offsets + 16 B edge_index + 4 B
-    edge_attr per edge. Each call includes its one 16-B (or 8-B) D2H read, the torch.nonzero sync."""
+    """process_adj (gnn.py:376-407) over this GPU's n*N per-ego graphs, two ways, on the same adjacency:
+    "count_pass": count kernel + hipcub scan + emit kernel (the adjacency read twice: the emit pass
+    re-reads it from beyond L2, profiles/r05_s42_edges_traffic.txt);
+    "one_pass": the step kernel also wrote each graph's nonzeros (LSM_OUT_ADJ_NNZ), and the call is
+    scan + emit (lsm_edges_scan_emit), the adjacency read once. step_fn(k) runs k more env steps with
+    pre-drawn actions (returns their event-timed ms per step); the step time with and without the counts
+    bound is measured alternately (what the counts cost the step). Algorithmic bytes: adjacency reads
+    (+ mask words, compact) + counts / offsets + 16 B edge_index + 4 B edge_attr per edge. Each call
+    includes its one D2H read of nnz, the torch.nonzero sync."""
     import ctypes as C
     import torch
     from lsm import capi, edges
@@ -154,16 +155,7 @@ def bench_edges(env, dev, step_fn, reps=50):
         return e0.elapsed_time(e1) / reps, nnz
 
     out = {"op": "GNNBase.process_adj (gnn.py:376-407) on the device", "envs": m, "graphs": B, "E": E}
-    ms, nnz = timed(None)
-    read = 2 * adj_read
-    written = nnz * 20 + (B + 2) * 8 + B * 8
-    out["count_pass"] = {"ms_per_call": ms, "nnz": nnz, "algorithmic_bytes": read + written,
-                         "achieved_GBps": (read + written) / (ms * 1e-3) / 1e9,
-                         "frac_hbm_peak": (read + written) / (ms * 1e-3) / 1e9 / PEAK_HBM_GBPS,
-                         "note": "count + scan + emit: the adjacency read twice (both reads counted)"}
-    if env.kernel_name.startswith("rollout_block_kernel"):
-        out["one_pass"] = None   # LSM_OUT_ADJ_NNZ: one-wave and team kernels (E <= 64)
-        return out
+    one = not env.kernel_name.startswith("rollout_block_kernel")   # LSM_OUT_ADJ_NNZ: E <= 64 kernels
     cnt = torch.zeros((env.num_envs, N), dtype=torch.int64, device=dev)
 
     def bind(t):
@@ -171,20 +163,26 @@ def bench_edges(env, dev, step_fn, reps=50):
                                            t.numel() * 8 if t is not None else 0), env.h)
 
     step_ms = {"with_counts": [], "without": []}
-    for _ in range(3):
-        for key, t in (("without", None), ("with_counts", cnt)):
-            bind(t)
-            step_fn(5)
-            torch.cuda.synchronize()
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            step_fn(50)
-            e1.record()
-            torch.cuda.synchronize()
-            step_ms[key].append(e0.elapsed_time(e1) / 50)
-    # the counts now belong to the last step's adjacency (the last loop ran with them bound)
+    if one:
+        for _ in range(3):
+            for key, t in (("without", None), ("with_counts", cnt)):
+                bind(t)
+                step_fn(5)
+                step_ms[key].append(step_fn(50))
+        # the last steps ran with the counts bound: cnt belongs to the current adjacency
+    ms, nnz = timed(None)
+    read = 2 * adj_read
+    written = nnz * 20 + (B + 2) * 8 + B * 8
+    out["count_pass"] = {"ms_per_call": ms, "nnz": nnz, "algorithmic_bytes": read + written,
+                         "achieved_GBps": (read + written) / (ms * 1e-3) / 1e9,
+                         "frac_hbm_peak": (read + written) / (ms * 1e-3) / 1e9 / PEAK_HBM_GBPS,
+                         "note": "count + scan + emit: the adjacency read twice (both reads counted)"}
+    if not one:
+        out["one_pass"] = None
+        return out
     ms1, nnz1 = timed(cnt[:m].reshape(-1))
     bind(None)
+    assert nnz1 == nnz
     read1 = adj_read + B * 8
     written1 = nnz1 * 20 + (B + 2) * 8
     out["one_pass"] = {"ms_per_call": ms1, "nnz": nnz1, "algorithmic_bytes": read1 + written1,
@@ -496,14 +494,16 @@ def main():
             "episode_summaries_timed": ep_summaries,
         }
         if a.edges:
-            extra = {"t": pre + a.steps}
-
             def more_steps(k):
-                for _ in range(k):
-                    t = extra["t"]
-                    env.step_async(synthetic_actions(t, rank * n_envs, n_envs, N, dev), ep)
+                # the window's pre-drawn actions again (the state has moved on; the step is the same work)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for t in range(k):
+                    env.step_async(acts_all[pre + t % a.steps], ep)
                     env.step_wait()
-                    extra["t"] = t + 1
+                e1.record()
+                torch.cuda.synchronize()
+                return e0.elapsed_time(e1) / k
             line["edges"] = bench_edges(env, dev, more_steps)
         print(json.dumps(line), flush=True)
     env.close()

@@ -1898,8 +1898,9 @@ __device__ __forceinline__ void emit_graph(const KParams& P, Lds& S, int env, bo
       adj_out[q] = (((m >> r) | (m >> c)) & 1ull) ? 0.0f : fv1(S, N, NL, E, r, c);
     }
   }
-  emit_nodes<DYN, LPE, NT>(P, S, env, uni);
+  // the counts read the thresholded table, which the node staging of emit_nodes overwrites (U1)
   if (gptr(P.o.adjnnz)) emit_adj_nnz<LPE, NT>(P, S, env);
+  emit_nodes<DYN, LPE, NT>(P, S, env, uni);
 }
 
 // node_obs [N][E][F] of one env (DI rows / airtaxi trig table already in LDS). `uni`: no

@@ -216,33 +216,52 @@ __device__ int random_scenario_wave2(const V& v, const ScenarioParams& p, double
   // chain; (2) agent i's draws on lane i; (3) the keep-previous / airtaxi-swap chain in agent order
   // (readlane, uniform); (4) headings, speeds, noise on lane i.
   const int after = 4 + (p.dyn == 0 ? 6 : 0) + 2;
-  int my_s = 0, my_acc = 0;
-  for (int i = 0; i < N; ++i) {
+  // try j (>= 0) of the agent whose block starts at word cs: accepted? (point 0 = words cs..cs+3)
+  auto accept = [&](int cs, int j) -> bool {
     uint32_t r[8];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) r[q] = v.raw(c + q);
+    for (int q = 0; q < 4; ++q) r[q] = v.raw(cs + q);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) r[4 + q] = v.raw(c + 4 + 4 * lane + q);
+    for (int q = 0; q < 4; ++q) r[4 + q] = v.raw(cs + 4 + 4 * j + q);
     const double ax = raw_uniform<V>(r[0], r[1], x0, x1), ay = raw_uniform<V>(r[2], r[3], y0, y1);
-    int acc = -1;
-    for (int base = 0; base < 1000 && acc < 0; base += 64) {
+    const double x = raw_uniform<V>(r[4], r[5], x0, x1), y = raw_uniform<V>(r[6], r[7], y0, y1);
+    const double dx = ax - x, dy = ay - y;
+    const double d = sqrt(dx * dx + dy * dy);
+    return (d > dmin && d < dmax) || j == 999;   // the 1000th try is kept whatever it is
+  };
+  // the first accepted try >= j0 of the agent at cs, 64 tries per ballot (the rare long loops)
+  auto first_from = [&](int cs, int j0) -> int {
+    for (int base = j0; base < 1000; base += 64) {
       const int j = base + lane;
-      if (base > 0) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) r[4 + q] = v.raw(c + 4 + 4 * j + q);
-      }
-      bool ok = false;
-      if (j < 1000) {
-        const double x = raw_uniform<V>(r[4], r[5], x0, x1), y = raw_uniform<V>(r[6], r[7], y0, y1);
-        const double dx = ax - x, dy = ay - y;
-        const double d = sqrt(dx * dx + dy * dy);
-        ok = (d > dmin && d < dmax) || j == 999;   // the 1000th try is kept whatever it is
-      }
-      const uint64_t m = __ballot(ok);
-      if (m) acc = base + __ffsll((unsigned long long)m) - 1;
+      const uint64_t m = __ballot(j < 1000 && accept(cs, j));
+      if (m) return base + __ffsll((unsigned long long)m) - 1;
     }
+    return 999;   // not reached: try 999 is always accepted
+  };
+  // Two agents per ballot: lanes 0-7 try 0-7 of agent i (block start c); lanes 8 + 8 g + t try t of
+  // agent i + 1 as if agent i accepted its try g (its block then starts after g + 1 tries), g < 7.
+  // One ballot gives acc_i (lowest set bit of lanes 0-7) and then, from group acc_i, acc_{i+1} --
+  // the chain of block starts resolves in half the rounds. A try beyond those (< 1 % at these
+  // acceptance rates) takes first_from. Same words, same arithmetic: the same acc as the sequential loop.
+  int my_s = 0, my_acc = 0;
+  for (int i = 0; i < N;) {
+    const int after_i = after - (i == 0 ? 4 : 0);
+    const bool two = i + 1 < N;
+    const int g = (lane - 8) >> 3;
+    const int cs = lane < 8 ? c : c + 4 + 4 * (g + 1) + after_i;
+    const int j = lane < 8 ? lane : (lane & 7);
+    const uint64_t m = __ballot((lane < 8 || two) && accept(cs, j));
+    int acc = (m & 0xffull) ? __ffsll((unsigned long long)(m & 0xffull)) - 1 : first_from(c, 8);
     if (lane == i) { my_s = c; my_acc = acc; }
-    c += 4 + 4 * (acc + 1) + after - (i == 0 ? 4 : 0);
+    c += 4 + 4 * (acc + 1) + after_i;
+    ++i;
+    if (two && acc < 7) {
+      const uint64_t mg = (m >> (8 + 8 * acc)) & 0xffull;
+      const int acc1 = mg ? __ffsll((unsigned long long)mg) - 1 : first_from(c, 8);
+      if (lane == i) { my_s = c; my_acc = acc1; }
+      c += 4 + 4 * (acc1 + 1) + after;
+      ++i;
+    }
   }
   DSTAMP(24);
   double dax = 0.0, day = 0.0, dbx = 0.0, dby = 0.0;
@@ -401,8 +420,13 @@ __device__ __forceinline__ void team_reset_finish(const KParams& P, Lds& S, int 
   reset_tail<DYN, 64, NT>(P, S, false);
 }
 
+// A/B variant builds may raise the airtaxi kernel's target (LSM_AB_AT_WPE=3: <= 168 VGPRs, the
+// register half of a third wave per SIMD; the LDS half needs <= 13.3 KB per env)
+#ifndef LSM_AB_AT_WPE
+#define LSM_AB_AT_WPE 2
+#endif
 template <int DYN, int NT, int G>
-__global__ __launch_bounds__(64 * G) __attribute__((amdgpu_waves_per_eu(DYN == 0 ? 4 : 2)))
+__global__ __launch_bounds__(64 * G) __attribute__((amdgpu_waves_per_eu(DYN == 0 ? 4 : LSM_AB_AT_WPE)))
 void rollout_team_kernel(const KParams* __restrict__ Pp, const KStep K) {
   static_assert(NT > 0 && G >= 2 && G * NT <= 64, "team: G envs x NT agents in one wave");
   constexpr int LPE = 64;
@@ -544,6 +568,9 @@ void rollout_team_kernel(const KParams* __restrict__ Pp, const KStep K) {
 #else
       GAS unsigned long long* ostp = nullptr;
 #endif
+      // (the gradient at the previous step's deconflicting agent, gathered speculatively with the pair
+      // values, served 98.65 % of the egos but lengthened the pair loop: 31.22 -> 32.47 us,
+      // profiles/r06_s03_ab_c3_gspec.txt)
       if (DYN == 0 && NT == 8) filter_prep_oct<8>(P, S, ostp);   // 32.66 -> 32.28 us (profiles/r05_v5_ab_c3_oct.txt)
       else if (lane < N) filter_prep<DYN, NT>(P, S, lane);
       TSTAMP(17);

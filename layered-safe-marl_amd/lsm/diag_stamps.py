@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--envs", type=int, default=0)
     ap.add_argument("--team", action="store_true",
                     help="the team kernel's stamps (lsm_team.h): phases A-E, work vs barrier wait")
+    ap.add_argument("--lib", default="", help="another stamps build (csrc/liblsm_rollout_<name>.so)")
     ap.add_argument("--kernel-select", default="",
                     help="lsm_kernel_select fields, e.g. team=2 (include/lsm_rollout.h; default: the library's choice)")
     ap.add_argument("--pick", default="",
@@ -42,7 +43,7 @@ def main():
         build_stamps()
         if a.build:
             return
-    os.environ["LSM_LIB"] = STAMP_LIB
+    os.environ["LSM_LIB"] = os.path.join(CSRC, a.lib) if a.lib else STAMP_LIB
     import numpy as np
     import torch
     sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))

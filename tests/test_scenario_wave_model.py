@@ -33,6 +33,80 @@ def uni(w, k, lo, hi):
     return lo + (hi - lo) * ((a * 67108864.0 + b) / 9007199254740992.0)
 
 
+def _accept(w, cs, j, box):
+    """Try j of the agent whose block starts at word cs (point 0 = words cs..cs+3): accepted?
+    (randomly_generate_separated_positions' test, utils.py:39-68; the 1000th try is kept)"""
+    x0, x1, y0, y1, dmin, dmax = box
+    ax, ay = uni(w, cs, x0, x1), uni(w, cs + 2, y0, y1)
+    x, y = uni(w, cs + 4 + 4 * j, x0, x1), uni(w, cs + 6 + 4 * j, y0, y1)
+    d = np.sqrt((ax - x) * (ax - x) + (ay - y) * (ay - y))
+    return (d > dmin and d < dmax) or j == 999
+
+
+def chain_sequential(w, N, c, box, after):
+    """The reference's order: agent after agent, try after try."""
+    starts, accs = [], []
+    for i in range(N):
+        acc = next(j for j in range(1000) if _accept(w, c, j, box))
+        starts.append(c)
+        accs.append(acc)
+        c += 4 + 4 * (acc + 1) + after - (4 if i == 0 else 0)
+    return starts, accs, c
+
+
+def chain_two_per_ballot(w, N, c, box, after):
+    """random_scenario_wave2's chain: one 64-lane ballot per two agents -- lanes 0-7 try 0-7 of agent
+    i, lanes 8 + 8 g + t try t of agent i + 1 as if agent i accepted try g (g < 7); tries past those
+    take 64-lane ballots from try 8 (first_from)."""
+    def first_from(cs, j0):
+        for base in range(j0, 1000, 64):
+            m = [j < 1000 and _accept(w, cs, j, box) for j in range(base, base + 64)]
+            if any(m):
+                return base + m.index(True)
+        return 999
+
+    starts, accs = [], []
+    i = 0
+    while i < N:
+        after_i = after - (4 if i == 0 else 0)
+        two = i + 1 < N
+        bits = []
+        for lane in range(64):
+            if lane < 8:
+                bits.append(_accept(w, c, lane, box))
+            else:
+                g, t = (lane - 8) >> 3, lane & 7
+                bits.append(two and _accept(w, c + 4 + 4 * (g + 1) + after_i, t, box))
+        acc = bits.index(True) if any(bits[:8]) else first_from(c, 8)
+        starts.append(c)
+        accs.append(acc)
+        c += 4 + 4 * (acc + 1) + after_i
+        i += 1
+        if two and acc < 7:
+            grp = bits[8 + 8 * acc: 16 + 8 * acc]
+            acc1 = grp.index(True) if any(grp) else first_from(c, 8)
+            starts.append(c)
+            accs.append(acc1)
+            c += 4 + 4 * (acc1 + 1) + after
+            i += 1
+    return starts, accs, c
+
+
+@pytest.mark.parametrize("N", [2, 3, 8, 9, 16])
+def test_chain_two_per_ballot(N):
+    """The two-agents-per-ballot chain equals the sequential rejection loops: the default boxes, and
+    narrow acceptance bands that make tries past 7 (both fallbacks) and acc = 7 (no group) common."""
+    w = raw_words(77 + N, 200000)
+    rng = np.random.default_rng(N)
+    boxes = [(-2.0, 2.0, -2.0, 2.0, 1.0, 3.0), (0.0, 4.5, -3.0, 3.0, 2.4, 4.8)]
+    for _ in range(6):   # narrow bands: acceptance 2-20 % per try
+        lo = rng.uniform(0.5, 2.5)
+        boxes.append((-2.0, 2.0, -2.0, 2.0, lo, lo + rng.uniform(0.02, 0.3)))
+    for box in boxes:
+        for c0, after in ((0, 12), (37, 6), (1001, 12)):
+            assert chain_two_per_ballot(w, N, c0, box, after) == chain_sequential(w, N, c0, box, after)
+
+
 def wave2_model(w, dyn, N, ws, cra, cr, crange, gsmin, gsmax):
     """random_scenario_wave2's algorithm, lane loops written as Python loops."""
     st = np.zeros((N, 4))
@@ -57,20 +131,10 @@ def wave2_model(w, dyn, N, ws, cra, cr, crange, gsmin, gsmax):
         x0, x1, y0, y1 = 0.0, 0.75 * ws, -yw * ws, yw * ws
         dmin, dmax = 0.5 * crange, crange
     after = 4 + (6 if dyn == 0 else 0) + 2
-    # (1) the chain of block starts: point 0, then the first accepted try (a ballot on the device)
-    starts, accs = [], []
-    for i in range(N):
-        ax, ay = uni(w, c, x0, x1), uni(w, c + 2, y0, y1)
-        acc = None
-        for j in range(1000):
-            x, y = uni(w, c + 4 + 4 * j, x0, x1), uni(w, c + 6 + 4 * j, y0, y1)
-            d = np.sqrt((ax - x) * (ax - x) + (ay - y) * (ay - y))
-            if (d > dmin and d < dmax) or j == 999:
-                acc = j
-                break
-        starts.append(c)
-        accs.append(acc)
-        c += 4 + 4 * (acc + 1) + after - (4 if i == 0 else 0)
+    box = (x0, x1, y0, y1, dmin, dmax)
+    # (1) the chain of block starts: point 0, then the first accepted try -- two agents per ballot on
+    # the device (chain_two_per_ballot), the same as the sequential loop (test_chain_two_per_ballot)
+    starts, accs, c = chain_two_per_ballot(w, N, c, box, after)
     # (2) every agent's draws on its lane
     draw, keep, mcs = [], [], []
     for i in range(N):
