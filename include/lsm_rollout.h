@@ -334,7 +334,9 @@ int lsm_host_scenario(const lsm_config* cfg, const lsm_curriculum* cur, uint32_t
  *                    no count pass: scan into offsets (int64 [B + 2]: offsets[B] = nnz, offsets[B + 1]
  *                    = the number of graphs whose nonzeros differed from their count, 0 when the
  *                    counts belong to `adj`; such a graph's slot is zero-filled) and emit as
- *                    lsm_edges_emit_dev does (nothing written when nnz > cap)
+ *                    lsm_edges_emit_dev does (nothing written when nnz > cap); host_nnz_bad (host
+ *                    int64 [2], nullable): the call then synchronises the stream and returns
+ *                    offsets[B], offsets[B + 1] there (torch.nonzero's one sync, no extra host call)
  * Errors: nonzero return, text in lsm_edges_last_error() (per host thread). */
 size_t lsm_edges_workspace_bytes(int64_t B);
 int lsm_edges_count(const float* adj, const uint64_t* masks, int64_t B, int32_t E, int32_t N,
@@ -347,7 +349,8 @@ int lsm_edges_emit_dev(const float* adj, const uint64_t* masks, int64_t B, int32
                        void* hip_stream);
 int lsm_edges_scan_emit(const float* adj, const uint64_t* masks, int64_t B, int32_t E, int32_t N,
                         const int64_t* counts, int64_t* offsets, void* workspace, size_t workspace_bytes,
-                        int64_t cap, int64_t* edge_index, float* edge_attr, void* hip_stream);
+                        int64_t cap, int64_t* edge_index, float* edge_attr, int64_t* host_nnz_bad,
+                        void* hip_stream);
 const char* lsm_edges_last_error(void);
 
 /* ---- Buffer insert: the derived rows of GMPERunner.insert / warmup (lsm_buffer.hip) ----------

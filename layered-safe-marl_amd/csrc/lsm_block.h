@@ -190,7 +190,11 @@ __device__ __forceinline__ void reset_block(const KParams& P, Lds& S, int env, c
 // went from 1240 to 1490 us per step (same-session A/B, profiles/r03_v14_bisect_c5.txt) when the
 // loop came in: 172 VGPRs instead of 165, so 2 waves per SIMD instead of 3. waves_per_eu(3) holds
 // the kernel to the 168 VGPRs of 3 waves.
-template <int DYN, int NT, bool NIS1>
+// REXT: the optional reward terms / shared reward may be on (P.rext). Config 5 (training default,
+// rext off) ran 1232 us with the rext block compiled in and 1206 us without it (same-session A/B,
+// profiles/r06_s05_ab_c5_bisect.txt: the round 3 -> 4 regression), so the host launches a REXT=false
+// instance when neither is configured.
+template <int DYN, int NT, bool NIS1, bool REXT>
 __global__ __launch_bounds__(BT) __attribute__((amdgpu_waves_per_eu(DYN == 0 ? 3 : 1)))
 void rollout_block_kernel(const KParams* __restrict__ Pp, const KStep K) {
   const KParams& P = *Pp;
@@ -492,7 +496,7 @@ void rollout_block_kernel(const KParams* __restrict__ Pp, const KStep K) {
   AgentTmp at;
   if (tid < N) reward_agent<DYN, NT>(P, S, env, tid, mag, at);
   __syncthreads();
-  if (P.rext) {   // optional reward terms / shared reward (reward_finish)
+  if (REXT && P.rext) {   // optional reward terms / shared reward (reward_finish)
     if (tid < N) reward_finish<DYN, NT>(P, S, env, tid, at);
     __syncthreads();
     if (P.collab && tid < N) reward_shared<NT>(P, S, env, tid);

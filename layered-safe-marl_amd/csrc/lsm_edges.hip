@@ -30,6 +30,7 @@
 #include <hipcub/device/device_scan.hpp>
 
 #include <cstdint>
+#include <type_traits>
 
 namespace {
 
@@ -75,29 +76,20 @@ __device__ __forceinline__ MaskRegs load_masks(const uint64_t* m, int W) {
   return M;
 }
 
-// bit r of the graph's disconnect words, by selects (no branch on the lane-varying word index)
-__device__ __forceinline__ uint32_t mbit(const MaskRegs& M, int r) {
+// bit r of the graph's disconnect words: an OR of masked words (no selection by index -- a select
+// chain over the words was rewritten into a dynamically indexed copy of them in LDS)
+__device__ __forceinline__ uint32_t mbit(const MaskRegs M, int r) {
   const uint32_t q = (uint32_t)r >> 6;
-  uint64_t x = M.w0;
-  x = q == 1u ? M.w1 : x;
-  x = q == 2u ? M.w2 : x;
-  x = q == 3u ? M.w3 : x;
+  const uint64_t x = (M.w0 & (0ull - (uint64_t)(q == 0u))) | (M.w1 & (0ull - (uint64_t)(q == 1u))) |
+                     (M.w2 & (0ull - (uint64_t)(q == 2u))) | (M.w3 & (0ull - (uint64_t)(q == 3u)));
   return (uint32_t)(x >> (r & 63)) & 1u;
 }
 
 // v, or +0.0 when row r or column c is disconnected (the reference assigns 0 to those entries,
 // navigation_graph_safe.py:976-989): an AND with an all-ones / all-zeros word, branch-free
-__device__ __forceinline__ float mask_val(float v, const MaskRegs& M, int r, int c) {
+__device__ __forceinline__ float mask_val(float v, const MaskRegs M, int r, int c) {
   const uint32_t drop = mbit(M, r) | mbit(M, c);
   return __uint_as_float(__float_as_uint(v) & (drop - 1u));
-}
-
-// Value of element k of graph b (0 where masked in the compact layout).
-__device__ __forceinline__ float load_val(const AdjSrc& s, const float* g, const MaskRegs& M, int k) {
-  const float v = __builtin_nontemporal_load(g + k);
-  if (!M.on) return v;
-  const int r = row_of(k, s.inv_e);
-  return mask_val(v, M, r, k - r * s.E);
 }
 
 __device__ __forceinline__ const float* graph_ptr(const AdjSrc& s, int64_t b) {
@@ -108,31 +100,45 @@ __device__ __forceinline__ const float* graph_ptr(const AdjSrc& s, int64_t b) {
 // VEC = 4 (E even, so every graph and row pair is 16-B aligned): each lane takes 4 consecutive
 // elements with one 16-B load; its nonzero count c in [0, 4] is spread over 3 ballots (bit k of c),
 // so the exclusive prefix over lanes is sum_k 2^k * popcount(ballot_k below the lane).
-template <int VEC>
-__device__ __forceinline__ int lane_vals(const AdjSrc& s, const float* g, const MaskRegs& M, int k, int EE,
-                                         float (&v)[VEC]) {
-  int c = 0;
-  if (VEC == 1) {
-    v[0] = k < EE ? load_val(s, g, M, k) : 0.0f;
-    c = v[0] != 0.0f;
-  } else {
-    if (k < EE) {
-      const f32x4 q = __builtin_nontemporal_load((const f32x4*)(g + k));
-      v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
-      if (M.on) {
+// A graph is walked in batches of CH chunks of WAVE * VEC elements: every chunk's load of a batch is
+// issued before the first is used, one memory round trip per batch rather than per chunk (E = 24:
+// the whole 576-element graph in one). Addresses are clamped into the graph (a chunk past EE re-reads
+// the graph's first elements, L2 hits) and values past EE zeroed by select.
+constexpr int CH = 4;
+
+template <int VEC, int NB>
+__device__ __forceinline__ void load_batch(const float* g, int k0, int EE, float (&v)[CH][VEC]) {
+  const int lane = lane_id();
+  typedef float f32x1 __attribute__((ext_vector_type(1)));
+  typedef typename std::conditional<VEC == 4, f32x4, f32x1>::type vec_t;
+  vec_t q[CH];
 #pragma unroll
-        for (int i = 0; i < VEC; ++i) {
-          const int r = row_of(k + i, s.inv_e);
-          v[i] = mask_val(v[i], M, r, k + i - r * s.E);
-        }
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < VEC; ++i) v[i] = 0.0f;
-    }
-#pragma unroll
-    for (int i = 0; i < VEC; ++i) c += v[i] != 0.0f;   // NaN counts, -0.0 does not (torch)
+  for (int h = 0; h < NB; ++h) {   // every load issued first: no use, no branch between them
+    const int k = k0 + h * WAVE * VEC + VEC * lane;
+    q[h] = __builtin_nontemporal_load((const vec_t*)(g + (k < EE ? k : 0)));
   }
+#pragma unroll
+  for (int h = 0; h < NB; ++h) {
+    const bool in = k0 + h * WAVE * VEC + VEC * lane < EE;
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) v[h][i] = in ? q[h][i] : 0.0f;
+  }
+}
+
+// the compact layout's disconnect masks applied (branch-free) to the lane's elements k .. k + VEC - 1
+// of a chunk, then their nonzero count (NaN counts, -0.0 does not: torch's nonzero)
+template <int VEC>
+__device__ __forceinline__ int mask_count(const AdjSrc& s, const MaskRegs M, int k, float (&v)[VEC]) {
+  if (M.on) {   // wave-uniform
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) {
+      const int r = row_of(k + i, s.inv_e);
+      v[i] = mask_val(v[i], M, r, k + i - r * s.E);
+    }
+  }
+  int c = 0;
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) c += v[i] != 0.0f;
   return c;
 }
 
@@ -140,7 +146,7 @@ __device__ __forceinline__ uint32_t below(uint64_t bal) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
 }
 
-template <int VEC>
+template <int VEC, int NB>
 __global__ __launch_bounds__(256) void edge_count_kernel(AdjSrc s, int64_t* __restrict__ counts,
                                                          int64_t* __restrict__ offsets) {
   const int64_t b = (int64_t)blockIdx.x * GRAPHS_PER_BLOCK + (threadIdx.x >> 6);
@@ -149,13 +155,17 @@ __global__ __launch_bounds__(256) void edge_count_kernel(AdjSrc s, int64_t* __re
   const MaskRegs M = load_masks(s.masks ? s.masks + b * s.W : nullptr, s.W);
   const int EE = s.E * s.E;
   int cnt = 0;
-  for (int k0 = 0; k0 < EE; k0 += WAVE * VEC) {
-    float v[VEC];
-    const int c = lane_vals<VEC>(s, g, M, k0 + VEC * lane_id(), EE, v);
-    if (VEC == 1) {
-      cnt += __popcll(__ballot(c != 0));
-    } else {
-      cnt += __popcll(__ballot(c & 1)) + 2 * __popcll(__ballot(c & 2)) + 4 * __popcll(__ballot(c & 4));
+  for (int k0 = 0; k0 < EE; k0 += WAVE * VEC * NB) {
+    float v[CH][VEC];
+    load_batch<VEC, NB>(g, k0, EE, v);
+#pragma unroll
+    for (int h = 0; h < NB; ++h) {
+      const int c = mask_count<VEC>(s, M, k0 + h * WAVE * VEC + VEC * lane_id(), v[h]);
+      if (VEC == 1) {
+        cnt += __popcll(__ballot(c != 0));
+      } else {
+        cnt += __popcll(__ballot(c & 1)) + 2 * __popcll(__ballot(c & 2)) + 4 * __popcll(__ballot(c & 4));
+      }
     }
   }
   if (lane_id() == 0) counts[b] = cnt;
@@ -171,7 +181,7 @@ __global__ __launch_bounds__(256) void edge_count_kernel(AdjSrc s, int64_t* __re
 // bad != nullptr: the offsets came from counts the caller supplied (the step kernel's
 // LSM_OUT_ADJ_NNZ), not from this file's count pass; a graph whose nonzeros differ from its slot
 // (offsets[b + 1] - offsets[b]) increments *bad, and its slot is zero-filled rather than left unset.
-template <int VEC>
+template <int VEC, int NB>
 __global__ __launch_bounds__(256) void edge_emit_kernel(AdjSrc s, const int64_t* __restrict__ offsets,
                                                         int64_t nnz, int64_t cap, int64_t* __restrict__ edge_index,
                                                         float* __restrict__ edge_attr, int64_t* __restrict__ bad) {
@@ -197,10 +207,16 @@ __global__ __launch_bounds__(256) void edge_emit_kernel(AdjSrc s, const int64_t*
     return;
   }
   int64_t found = 0;   // the graph's nonzeros (checked against its slot when the counts are given)
-  for (int k0 = 0; k0 < EE && (bad || pos < end); k0 += WAVE * VEC) {
+  for (int kb = 0; kb < EE && (bad || pos < end); kb += WAVE * VEC * NB) {
+  float vb[CH][VEC];
+  load_batch<VEC, NB>(g, kb, EE, vb);
+#pragma unroll
+  for (int h = 0; h < NB; ++h) {
+    const int k0 = kb + h * WAVE * VEC;
+    if (k0 >= EE || !(bad || pos < end)) break;   // wave-uniform
     const int k = k0 + VEC * lane;
-    float v[VEC];
-    const int c = lane_vals<VEC>(s, g, M, k, EE, v);
+    float (&v)[VEC] = vb[h];
+    const int c = mask_count<VEC>(s, M, k, v);
     uint32_t pre;
     int tot;
     if (VEC == 1) {
@@ -239,6 +255,7 @@ __global__ __launch_bounds__(256) void edge_emit_kernel(AdjSrc s, const int64_t*
     __builtin_amdgcn_wave_barrier();   // slots are rewritten by the next chunk
     pos += room;
   }
+  }
   if (bad && found != end - pos0) {
     for (int64_t t = pos + lane; t < end; t += WAVE) {   // a short graph: its slot's tail zeroed
       edge_index[t] = 0;
@@ -255,6 +272,26 @@ __global__ void offsets_init_kernel(int64_t* offsets, int64_t B) {
     offsets[0] = 0;
     offsets[B + 1] = 0;
   }
+}
+
+// chunks per memory round trip of the compact layout's kernels (the reference layout's: CH)
+#ifndef LSM_EDGES_COMPACT_NB
+#define LSM_EDGES_COMPACT_NB CH
+#endif
+template <int VEC>
+void launch_count(const AdjSrc& s, int64_t blocks, int64_t* counts, int64_t* offsets, hipStream_t st) {
+  if (s.masks) edge_count_kernel<VEC, LSM_EDGES_COMPACT_NB><<<dim3((unsigned)blocks), 256, 0, st>>>(s, counts, offsets);
+  else edge_count_kernel<VEC, CH><<<dim3((unsigned)blocks), 256, 0, st>>>(s, counts, offsets);
+}
+
+template <int VEC>
+void launch_emit(const AdjSrc& s, int64_t blocks, const int64_t* offsets, int64_t nnz, int64_t cap,
+                 int64_t* edge_index, float* edge_attr, int64_t* bad, hipStream_t st) {
+  if (s.masks)
+    edge_emit_kernel<VEC, LSM_EDGES_COMPACT_NB><<<dim3((unsigned)blocks), 256, 0, st>>>(s, offsets, nnz, cap, edge_index,
+                                                                                    edge_attr, bad);
+  else
+    edge_emit_kernel<VEC, CH><<<dim3((unsigned)blocks), 256, 0, st>>>(s, offsets, nnz, cap, edge_index, edge_attr, bad);
 }
 
 thread_local char g_err[256];
@@ -312,8 +349,8 @@ int lsm_edges_count(const float* adj, const uint64_t* masks, int64_t B, int32_t 
   void* temp = (char*)workspace + cbytes;
   size_t tbytes = workspace_bytes - cbytes;
   const int64_t blocks = (B + GRAPHS_PER_BLOCK - 1) / GRAPHS_PER_BLOCK;
-  if (E % 2 == 0) edge_count_kernel<4><<<dim3((unsigned)blocks), 256, 0, st>>>(s, counts, offsets);
-  else edge_count_kernel<1><<<dim3((unsigned)blocks), 256, 0, st>>>(s, counts, offsets);
+  if (E % 2 == 0) launch_count<4>(s, blocks, counts, offsets, st);
+  else launch_count<1>(s, blocks, counts, offsets, st);
   if (hipcub::DeviceScan::InclusiveSum(temp, tbytes, counts, offsets + 1, (int)B, st) != hipSuccess)
     return fail("scan failed");
   return hipGetLastError() == hipSuccess ? 0 : fail("launch failed");
@@ -330,11 +367,9 @@ int lsm_edges_emit(const float* adj, const uint64_t* masks, int64_t B, int32_t E
   if (B == 0 || nnz == 0) return 0;
   const int64_t blocks = (B + GRAPHS_PER_BLOCK - 1) / GRAPHS_PER_BLOCK;
   if (E % 2 == 0)
-    edge_emit_kernel<4><<<dim3((unsigned)blocks), 256, 0, (hipStream_t)stream>>>(s, offsets, nnz, nnz, edge_index,
-                                                                                 edge_attr, nullptr);
+    launch_emit<4>(s, blocks, offsets, nnz, nnz, edge_index, edge_attr, nullptr, (hipStream_t)stream);
   else
-    edge_emit_kernel<1><<<dim3((unsigned)blocks), 256, 0, (hipStream_t)stream>>>(s, offsets, nnz, nnz, edge_index,
-                                                                                 edge_attr, nullptr);
+    launch_emit<1>(s, blocks, offsets, nnz, nnz, edge_index, edge_attr, nullptr, (hipStream_t)stream);
   return hipGetLastError() == hipSuccess ? 0 : fail("launch failed");
 }
 
@@ -349,17 +384,32 @@ int lsm_edges_emit_dev(const float* adj, const uint64_t* masks, int64_t B, int32
   if (B == 0 || cap == 0) return 0;
   const int64_t blocks = (B + GRAPHS_PER_BLOCK - 1) / GRAPHS_PER_BLOCK;
   if (E % 2 == 0)
-    edge_emit_kernel<4><<<dim3((unsigned)blocks), 256, 0, (hipStream_t)stream>>>(s, offsets, -1, cap, edge_index,
-                                                                                 edge_attr, nullptr);
+    launch_emit<4>(s, blocks, offsets, -1, cap, edge_index, edge_attr, nullptr, (hipStream_t)stream);
   else
-    edge_emit_kernel<1><<<dim3((unsigned)blocks), 256, 0, (hipStream_t)stream>>>(s, offsets, -1, cap, edge_index,
-                                                                                 edge_attr, nullptr);
+    launch_emit<1>(s, blocks, offsets, -1, cap, edge_index, edge_attr, nullptr, (hipStream_t)stream);
   return hipGetLastError() == hipSuccess ? 0 : fail("launch failed");
+}
+
+// offsets[B], offsets[B + 1] -> host through a per-thread pinned staging pair: a D2H copy into
+// pageable memory is staged by the runtime (a second synchronisation and a host copy) -- the one-pass
+// call's host time (profiles/r06_s05_bench_edges.json: 34 us of 101 us per call)
+static int read_pair(const int64_t* dev, int64_t* host, hipStream_t st) {
+  static thread_local int64_t* pinned = nullptr;
+  if (!pinned && hipHostMalloc((void**)&pinned, 2 * sizeof(int64_t), hipHostMallocDefault) != hipSuccess) {
+    pinned = nullptr;
+    return fail("pinned staging allocation failed");
+  }
+  if (hipMemcpyAsync(pinned, dev, 2 * sizeof(int64_t), hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess)
+    return fail("reading the edge count failed");
+  host[0] = pinned[0];
+  host[1] = pinned[1];
+  return 0;
 }
 
 int lsm_edges_scan_emit(const float* adj, const uint64_t* masks, int64_t B, int32_t E, int32_t N,
                         const int64_t* counts, int64_t* offsets, void* workspace, size_t workspace_bytes, int64_t cap,
-                        int64_t* edge_index, float* edge_attr, void* stream) {
+                        int64_t* edge_index, float* edge_attr, int64_t* host_nnz_bad, void* stream) {
   AdjSrc s;
   if (make_src(adj, masks, B, E, N, &s)) return 1;
   if (B > INT32_MAX) return fail("B exceeds the scan's int32 item count");
@@ -369,7 +419,10 @@ int lsm_edges_scan_emit(const float* adj, const uint64_t* masks, int64_t B, int3
   if (workspace_bytes < lsm_edges_workspace_bytes(B)) return fail("workspace too small");
   hipStream_t st = (hipStream_t)stream;
   offsets_init_kernel<<<1, 64, 0, st>>>(offsets, B);
-  if (B == 0) return hipGetLastError() == hipSuccess ? 0 : fail("launch failed");
+  if (B == 0) {
+    if (hipGetLastError() != hipSuccess) return fail("launch failed");
+    return host_nnz_bad ? read_pair(offsets, host_nnz_bad, st) : 0;
+  }
   const size_t cbytes = ((size_t)B * sizeof(int64_t) + 255) & ~(size_t)255;
   void* temp = (char*)workspace + cbytes;
   size_t tbytes = workspace_bytes - cbytes;
@@ -379,13 +432,13 @@ int lsm_edges_scan_emit(const float* adj, const uint64_t* masks, int64_t B, int3
     const int64_t blocks = (B + GRAPHS_PER_BLOCK - 1) / GRAPHS_PER_BLOCK;
     // the scan above rewrote offsets[B]; the error word offsets[B + 1] was cleared before it
     if (E % 2 == 0)
-      edge_emit_kernel<4><<<dim3((unsigned)blocks), 256, 0, st>>>(s, offsets, -1, cap, edge_index, edge_attr,
-                                                                  offsets + B + 1);
+      launch_emit<4>(s, blocks, offsets, -1, cap, edge_index, edge_attr, offsets + B + 1, st);
     else
-      edge_emit_kernel<1><<<dim3((unsigned)blocks), 256, 0, st>>>(s, offsets, -1, cap, edge_index, edge_attr,
-                                                                  offsets + B + 1);
+      launch_emit<1>(s, blocks, offsets, -1, cap, edge_index, edge_attr, offsets + B + 1, st);
   }
-  return hipGetLastError() == hipSuccess ? 0 : fail("launch failed");
+  if (hipGetLastError() != hipSuccess) return fail("launch failed");
+  // the call's one synchronisation (torch.nonzero's): offsets[B], offsets[B + 1]
+  return host_nnz_bad ? read_pair(offsets + B, host_nnz_bad, st) : 0;
 }
 
 }  // extern "C"

@@ -3566,23 +3566,26 @@ int launch_team_t(lsm_env* e, const KStep& L, size_t env_bytes, hipStream_t st) 
   return 0;
 }
 
-template <int DYN, int NT, bool NIS1>
+template <int DYN, int NT, bool NIS1, bool REXT>
 int launch_block_nis(lsm_env* e, const KStep& L, size_t env_lds, hipStream_t st) {
   static bool attr = false;   // LDS above the 64 KB default needs an explicit opt-in
   if (!attr && env_lds > 65536) {
-    HIPCHK(e, hipFuncSetAttribute((const void*)rollout_block_kernel<DYN, NT, NIS1>,
+    HIPCHK(e, hipFuncSetAttribute((const void*)rollout_block_kernel<DYN, NT, NIS1, REXT>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)env_lds));
     attr = true;
   }
-  hipLaunchKernelGGL((rollout_block_kernel<DYN, NT, NIS1>), dim3(e->cfg.num_envs), dim3(BT), env_lds, st,
+  hipLaunchKernelGGL((rollout_block_kernel<DYN, NT, NIS1, REXT>), dim3(e->cfg.num_envs), dim3(BT), env_lds, st,
                      active_params(e), L);
   return 0;
 }
 
 template <int DYN, int NT>
 int launch_block_t(lsm_env* e, const KStep& L, size_t env_lds, hipStream_t st) {
-  return e->cfg.num_internal_step > 1 ? launch_block_nis<DYN, NT, false>(e, L, env_lds, st)
-                                      : launch_block_nis<DYN, NT, true>(e, L, env_lds, st);
+  if (e->cfg.num_internal_step > 1) return launch_block_nis<DYN, NT, false, true>(e, L, env_lds, st);
+  // fill_params' P.rext: reward_finish / reward_shared run only then
+  const bool rext = e->cfg.reward_terms != 0 || e->cfg.collaborative;
+  return rext ? launch_block_nis<DYN, NT, true, true>(e, L, env_lds, st)
+              : launch_block_nis<DYN, NT, true, false>(e, L, env_lds, st);
 }
 
 

@@ -114,7 +114,7 @@ def load_library(path: str = LIB_PATH):
         "lsm_edges_count": (I32, [P, P, I64, I32, I32, P, P, SZ, P]),
         "lsm_edges_emit": (I32, [P, P, I64, I32, I32, P, I64, P, P, P]),
         "lsm_edges_emit_dev": (I32, [P, P, I64, I32, I32, P, I64, P, P, P]),
-        "lsm_edges_scan_emit": (I32, [P, P, I64, I32, I32, P, P, P, SZ, I64, P, P, P]),
+        "lsm_edges_scan_emit": (I32, [P, P, I64, I32, I32, P, P, P, SZ, I64, P, P, P, P]),
         "lsm_edges_last_error": (C.c_char_p, []),
         "lsm_bind_output_ring": (I32, [P, I32, P, SZ, I32, I32]),
         "lsm_select_ring": (I32, [P, I32]),

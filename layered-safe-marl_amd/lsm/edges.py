@@ -94,10 +94,11 @@ def _run(adj, masks, B, E, N, counts=None):
         counts = counts.contiguous()
         ebuf = torch.empty(2 * max(cap, 1), dtype=torch.int64, device=dev)
         abuf = torch.empty(max(cap, 1), dtype=torch.float32, device=dev)
+        host = (C.c_int64 * 2)()   # nnz, mismatched graphs: read back by the call itself (the one sync)
         _check(lib.lsm_edges_scan_emit(ap, mp, B, E, N, C.c_void_p(counts.data_ptr()),
                                        C.c_void_p(offsets.data_ptr()), C.c_void_p(ws.data_ptr()), ws_bytes, cap,
-                                       C.c_void_p(ebuf.data_ptr()), C.c_void_p(abuf.data_ptr()), stream), lib)
-        nnz, bad = (int(x) for x in offsets[B:B + 2].tolist())   # the one sync
+                                       C.c_void_p(ebuf.data_ptr()), C.c_void_p(abuf.data_ptr()), host, stream), lib)
+        nnz, bad = int(host[0]), int(host[1])
         if nnz > cap:
             raise EdgeError("edge count %d exceeds B*E*E = %d" % (nnz, cap))
         if bad:

@@ -81,5 +81,52 @@ def main():
                     print("     got ", gg[:, d[0]:d[0] + 6].T.tolist())
 
 
+def config3_compact(libs):
+    """BASELINE config 3's compact adjacency after 40 steps (disconnect bits in many graphs): per-graph
+    counts and the emitted edges of each library against the oracle (test_gpu_env_edge_list_full_size)."""
+    import torch
+    from lsm import hj_tables
+    from lsm.config import EnvArgs
+    from lsm.vec_env import GpuGraphVecEnv
+    from oracle.process_adj import process_adj as ora
+    args = EnvArgs(num_agents=8, num_env_steps=250 * 4, use_safety_filter=True, seed=0)
+    vt, _ = hj_tables.default_tables("double_integrator", small=True)
+    env = GpuGraphVecEnv(args, num_envs=4096, device="cuda:0", value_table=vt, return_numpy=False,
+                         build_infos=False, adj_layout="compact")
+    env.reset(4)
+    g = torch.Generator(device="cuda:0").manual_seed(3)
+    for _ in range(40):
+        env.step(torch.randint(0, 25, (4096, 8), generator=g, device="cuda:0", dtype=torch.int32), 4)
+    E, N, B = env.E, env.N, 4096 * 8
+    ref = env.reference_adj().reshape(-1, E, E).cpu().numpy()
+    want_cnt = (ref != 0).reshape(B, -1).sum(axis=1)
+    wei, _ = ora(ref)
+    st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    for name, lib in libs:
+        for rep in range(3):
+            wsb = int(lib.lsm_edges_workspace_bytes(B))
+            ws = torch.empty(wsb, dtype=torch.uint8, device="cuda")
+            off = torch.zeros(B + 2, dtype=torch.int64, device="cuda")
+            assert lib.lsm_edges_count(C.c_void_p(env.t_adj.data_ptr()), C.c_void_p(env.t_adj_mask.data_ptr()), B, E, N,
+                                       C.c_void_p(off.data_ptr()), C.c_void_p(ws.data_ptr()), wsb, st) == 0
+            o = off.cpu().numpy()[:B + 1]
+            badc = np.nonzero(np.diff(o) != want_cnt)[0]
+            nnz = int(o[B])
+            ei = torch.zeros((2, nnz), dtype=torch.int64, device="cuda")
+            ea = torch.zeros((nnz, 1), dtype=torch.float32, device="cuda")
+            assert lib.lsm_edges_emit(C.c_void_p(env.t_adj.data_ptr()), C.c_void_p(env.t_adj_mask.data_ptr()), B, E, N,
+                                      C.c_void_p(off.data_ptr()), nnz, C.c_void_p(ei.data_ptr()),
+                                      C.c_void_p(ea.data_ptr()), st) == 0
+            gei = ei.cpu().numpy()
+            bad_e = int((gei != wei).any(axis=0).sum()) if gei.shape == wei.shape else -1
+            print("%s config-3 compact call %d: count-bad graphs %d, emit-bad edges %d" % (name, rep, len(badc), bad_e),
+                  flush=True)
+    env.close()
+
+
 if __name__ == "__main__":
     main()
+    import ctypes as _C
+    from lsm import capi as _capi
+    libs = [("cur", bind(_capi.load_library()))] + [(os.path.basename(p), bind(_C.CDLL(p))) for p in sys.argv[1:]]
+    config3_compact(libs)
