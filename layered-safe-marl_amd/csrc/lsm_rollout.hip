@@ -369,7 +369,8 @@ __device__ __forceinline__ GAS T* gptr(T* p) {
 // the filter on: 37.9 vs 35.9 us per step at config 3.)
 // Output stores. NTS = nontemporal (`nt`): measured on MI355X (profiles/r01_v9_nt_stores.txt)
 // +5 % at config 4 (airtaxi N = 16) and +8.5 % at config 5 (workgroup kernel), within noise
-// (-1 %) at config 3, so the N >= 16 one-wave kernels and the workgroup kernel use it.
+// (-1 %) at config 3, so the N >= 16 one-wave kernels and the workgroup kernel use it. The N = 8
+// team kernel with them: 34.82 vs 31.50 us at config 3 (profiles/r06_s07_ab_c3.txt).
 template <bool NTS = false>
 __device__ __forceinline__ void st_stream(GAS float* dst, float4 v) {
   const f32x4 x = {v.x, v.y, v.z, v.w};
@@ -3551,17 +3552,20 @@ void launch_t(lsm_env* e, const KStep& L, size_t env_lds, hipStream_t st) {
                      active_params(e), L);
 }
 
-template <int DYN, int NT, int G>
+template <int DYN, int NT, int G, bool REXT>
 int launch_team_t(lsm_env* e, const KStep& L, size_t env_bytes, hipStream_t st) {
   static bool attr = false;   // LDS above the 64 KB default needs an explicit opt-in
-  const size_t lds = env_bytes * G;
+#ifndef LSM_AB_LDS_PAD   // A/B variant builds only: extra LDS per workgroup (fewer workgroups per CU)
+#define LSM_AB_LDS_PAD 0
+#endif
+  const size_t lds = env_bytes * G + LSM_AB_LDS_PAD;
   if (!attr && lds > 65536) {
-    HIPCHK(e, hipFuncSetAttribute((const void*)rollout_team_kernel<DYN, NT, G>,
+    HIPCHK(e, hipFuncSetAttribute((const void*)rollout_team_kernel<DYN, NT, G, REXT>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     attr = true;
   }
   const int blocks = (e->cfg.num_envs + G - 1) / G;
-  hipLaunchKernelGGL((rollout_team_kernel<DYN, NT, G>), dim3(blocks), dim3(WAVE * G), lds, st,
+  hipLaunchKernelGGL((rollout_team_kernel<DYN, NT, G, REXT>), dim3(blocks), dim3(WAVE * G), lds, st,
                      active_params(e), L);
   return 0;
 }
@@ -3595,18 +3599,21 @@ int launch_block_t(lsm_env* e, const KStep& L, size_t env_lds, hipStream_t st) {
 // is one translation unit (diagnostic builds).
 #define LSM_G1(X) X(0, 64, 0) X(0, 32, 0) X(0, 16, 0) X(0, 32, 8) X(0, 64, 3) X(0, 64, 8)
 #define LSM_G2(X) X(1, 64, 0) X(1, 32, 0) X(1, 16, 0) X(1, 32, 16) X(1, 64, 3) X(1, 64, 16)
-#define LSM_G3(X) X(0, 8, 8) X(0, 8, 4) X(0, 8, 2)
-#define LSM_G4(X) X(1, 16, 4) X(1, 16, 2)
+#define LSM_G3(X) X(0, 8, 8, false) X(0, 8, 4, false) X(0, 8, 2, false)
+#define LSM_G4(X) X(1, 16, 4, false) X(1, 16, 2, false)
+#define LSM_G7(X) X(0, 8, 8, true) X(0, 8, 4, true) X(0, 8, 2, true)
+#define LSM_G8(X) X(1, 16, 4, true) X(1, 16, 2, true)
 #define LSM_G5(X) X(0, 64) X(0, 0)
 #define LSM_G6(X) X(1, 64) X(1, 0)
 #define LSM_RT(a, b, c) template void launch_t<a, b, c>(lsm_env*, const KStep&, size_t, hipStream_t);
-#define LSM_TT(a, b, c) template int launch_team_t<a, b, c>(lsm_env*, const KStep&, size_t, hipStream_t);
+#define LSM_TT(a, b, c, r) template int launch_team_t<a, b, c, r>(lsm_env*, const KStep&, size_t, hipStream_t);
 #define LSM_BK(a, b) template int launch_block_t<a, b>(lsm_env*, const KStep&, size_t, hipStream_t);
 #define LSM_RT_E(a, b, c) extern LSM_RT(a, b, c)
-#define LSM_TT_E(a, b, c) extern LSM_TT(a, b, c)
+#define LSM_TT_E(a, b, c, r) extern LSM_TT(a, b, c, r)
 #define LSM_BK_E(a, b) extern LSM_BK(a, b)
 #if defined(LSM_PART) && LSM_PART == 0
 LSM_G1(LSM_RT_E) LSM_G2(LSM_RT_E) LSM_G3(LSM_TT_E) LSM_G4(LSM_TT_E) LSM_G5(LSM_BK_E) LSM_G6(LSM_BK_E)
+LSM_G7(LSM_TT_E) LSM_G8(LSM_TT_E)
 #elif defined(LSM_PART) && LSM_PART == 1
 LSM_G1(LSM_RT)
 #elif defined(LSM_PART) && LSM_PART == 2
@@ -3619,6 +3626,10 @@ LSM_G4(LSM_TT)
 LSM_G5(LSM_BK)
 #elif defined(LSM_PART) && LSM_PART == 6
 LSM_G6(LSM_BK)
+#elif defined(LSM_PART) && LSM_PART == 7
+LSM_G7(LSM_TT)
+#elif defined(LSM_PART) && LSM_PART == 8
+LSM_G8(LSM_TT)
 #endif
 
 #if LSM_HOST_PART
@@ -4261,13 +4272,15 @@ static int launch(lsm_env* e, KStep& L, hipStream_t st) {
   }
   if (e->team) {
     int rc = 1;
+    // fill_params' P.rext: the kernel without the optional-reward block unless it can run
+    const bool rext = e->cfg.reward_terms != 0 || e->cfg.collaborative;
     if (di) {
-      if (e->team == 8) rc = launch_team_t<0, 8, 8>(e, L, env_lds, st);
-      else if (e->team == 4) rc = launch_team_t<0, 8, 4>(e, L, env_lds, st);
-      else rc = launch_team_t<0, 8, 2>(e, L, env_lds, st);
+      if (e->team == 8) rc = rext ? launch_team_t<0, 8, 8, true>(e, L, env_lds, st) : launch_team_t<0, 8, 8, false>(e, L, env_lds, st);
+      else if (e->team == 4) rc = rext ? launch_team_t<0, 8, 4, true>(e, L, env_lds, st) : launch_team_t<0, 8, 4, false>(e, L, env_lds, st);
+      else rc = rext ? launch_team_t<0, 8, 2, true>(e, L, env_lds, st) : launch_team_t<0, 8, 2, false>(e, L, env_lds, st);
     } else {
-      if (e->team == 4) rc = launch_team_t<1, 16, 4>(e, L, env_lds, st);
-      else rc = launch_team_t<1, 16, 2>(e, L, env_lds, st);
+      if (e->team == 4) rc = rext ? launch_team_t<1, 16, 4, true>(e, L, env_lds, st) : launch_team_t<1, 16, 4, false>(e, L, env_lds, st);
+      else rc = rext ? launch_team_t<1, 16, 2, true>(e, L, env_lds, st) : launch_team_t<1, 16, 2, false>(e, L, env_lds, st);
     }
     if (rc) return rc;
     HIPCHK(e, hipGetLastError());
@@ -4317,11 +4330,15 @@ const char* lsm_kernel_name(const lsm_env* e) {
   if (!e) return "";
   const bool di = e->cfg.dynamics == LSM_DOUBLE_INTEGRATOR;
   const int D = di ? 0 : 1;
+  const char* rext = (e->cfg.reward_terms != 0 || e->cfg.collaborative) ? "true" : "false";
   if (e->block) {
     const bool spec64 = e->N == 64 && e->L == 2 && !e->generic_only;
-    name = "rollout_block_kernel<" + std::to_string(D) + ", " + std::to_string(spec64 ? 64 : 0) + ">";
+    const bool nis1 = e->cfg.num_internal_step <= 1;
+    name = "rollout_block_kernel<" + std::to_string(D) + ", " + std::to_string(spec64 ? 64 : 0) + ", " +
+           (nis1 ? "true" : "false") + ", " + (nis1 ? rext : "true") + ">";
   } else if (e->team) {
-    name = "rollout_team_kernel<" + std::to_string(D) + ", " + std::to_string(e->N) + ", " + std::to_string(e->team) + ">";
+    name = "rollout_team_kernel<" + std::to_string(D) + ", " + std::to_string(e->N) + ", " + std::to_string(e->team) +
+           ", " + rext + ">";
   } else {
     const bool specN = e->L == 2 && !e->generic_only &&
                        ((e->lpe == 64 && ((di && (e->N == 3 || e->N == 8)) || (!di && (e->N == 3 || e->N == 16)))) ||

@@ -420,13 +420,21 @@ __device__ __forceinline__ void team_reset_finish(const KParams& P, Lds& S, int 
   reset_tail<DYN, 64, NT>(P, S, false);
 }
 
-// A/B variant builds may raise the airtaxi kernel's target (LSM_AB_AT_WPE=3: <= 168 VGPRs, the
-// register half of a third wave per SIMD; the LDS half needs <= 13.3 KB per env)
+// The airtaxi kernel is held to 2 waves per SIMD both ways: its LDS allows no more (2 workgroups
+// of 4 x 19.3 KB per CU), and with the upper bound open the compiler scheduled for 3 (135 VGPRs):
+// 396.3 us per step at config 4 against 387.5 capped at 2 (224 VGPRs; profiles/r06_s08_ab_c4.txt).
+// A/B variant builds may move either bound (LSM_AB_AT_WPE, LSM_AB_AT_WPE_MAX).
 #ifndef LSM_AB_AT_WPE
 #define LSM_AB_AT_WPE 2
 #endif
-template <int DYN, int NT, int G>
-__global__ __launch_bounds__(64 * G) __attribute__((amdgpu_waves_per_eu(DYN == 0 ? 4 : LSM_AB_AT_WPE)))
+#ifndef LSM_AB_AT_WPE_MAX
+#define LSM_AB_AT_WPE_MAX 2
+#endif
+// REXT: the optional reward terms / shared reward may be on (P.rext); the host launches REXT = false
+// when neither is configured. Compiled in, that block cost <0, 8, 4> 92 B of scratch per lane (spills
+// across the whole kernel, 0 B without it; profiles/r06_s07_ab_c3.txt).
+template <int DYN, int NT, int G, bool REXT>
+__global__ __launch_bounds__(64 * G) __attribute__((amdgpu_waves_per_eu(DYN == 0 ? 4 : LSM_AB_AT_WPE, DYN == 0 ? 8 : LSM_AB_AT_WPE_MAX)))
 void rollout_team_kernel(const KParams* __restrict__ Pp, const KStep K) {
   static_assert(NT > 0 && G >= 2 && G * NT <= 64, "team: G envs x NT agents in one wave");
   constexpr int LPE = 64;
@@ -681,7 +689,7 @@ void rollout_team_kernel(const KParams* __restrict__ Pp, const KStep K) {
       reward_agent<DYN, NT>(P, A, aenv, ai, mag, at);
     }
     esync<LPE>();   // every agent's goal / done update before the snapshot masks
-    if (P.rext) {   // optional reward terms / shared reward (reward_finish)
+    if (REXT && P.rext) {   // optional reward terms / shared reward (reward_finish)
       if (alane) reward_finish<DYN, NT>(P, A, aenv, ai, at);
       esync<LPE>();
       if (P.collab && alane) reward_shared<NT>(P, A, aenv, ai);

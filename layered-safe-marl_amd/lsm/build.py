@@ -18,7 +18,7 @@ SRC = os.path.join(CSRC, "lsm_rollout.hip")   # the rollout TU
 OUT = os.path.join(CSRC, "liblsm_rollout.so")
 HDR = os.path.join(os.path.dirname(os.path.dirname(HERE)), "include", "lsm_rollout.h")
 ROLLOUT_DEPS = ["lsm_numeric.h", "lsm_scenario.h", "lsm_block.h", "lsm_rk45.h", "lsm_pow_tables.h", "lsm_team.h"]
-ROLLOUT_PARTS = 7
+ROLLOUT_PARTS = 9
 # the other translation units -> their dependencies (each compiled to its own object, then linked)
 UNITS = {
     "lsm_edges.hip": [],
