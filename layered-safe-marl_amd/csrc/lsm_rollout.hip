@@ -208,6 +208,8 @@ struct KParams {
   double dt, world_size, coord_range, world_eng, sep_target, max_speed, min_speed, gs_min, gs_max;
   double coord_range_s;  // the largest double s with sqrt(s) <= coord_range (correctly rounded sqrt):
                          // sqrt(s) > coord_range <=> s > coord_range_s, for squared distances s >= 0
+  double scen_d2lo, scen_d2hi;   // the scenario's separated-positions band (dmin, dmax) on squared
+                                 // distances: sqrt(s) > dmin <=> s > d2lo, sqrt(s) < dmax <=> s < d2hi
   double act0[5], act1[5];
   double mag_c[50], mag_s[50];
   double cos_pi6, two_pi, pi;
@@ -2273,6 +2275,7 @@ __device__ __forceinline__ ScenarioParams scenario_params(const KParams& P, cons
   sp.dyn = DYN; sp.N = N; sp.L = L; sp.world_size = P.world_size; sp.coordination_range = P.coord_range;
   sp.goal_speed_min = P.gs_min; sp.goal_speed_max = P.gs_max;
   sp.ratio_airtaxi = S.cur[C_RAT]; sp.ratio_scenario = S.cur[C_RSC]; sp.two_pi = P.two_pi; sp.pi = P.pi;
+  sp.d2lo = P.scen_d2lo; sp.d2hi = P.scen_d2hi;
   return sp;
 }
 
@@ -3684,6 +3687,18 @@ static void fill_params(const lsm_env* e, KParams& P) {
     while (std::sqrt(std::nextafter(t, INFINITY)) <= P.coord_range) t = std::nextafter(t, INFINITY);
     P.coord_range_s = t;
   }
+  {   // random_scenario_wave2's band, the device's products (lsm_team.h)
+    const double dmin = di ? 0.25 * P.coord_range : 0.5 * P.coord_range;
+    const double dmax = di ? 0.75 * P.coord_range : P.coord_range;
+    double lo = dmin * dmin;
+    while (std::sqrt(lo) > dmin) lo = std::nextafter(lo, 0.0);
+    while (std::sqrt(std::nextafter(lo, INFINITY)) <= dmin) lo = std::nextafter(lo, INFINITY);
+    double hi = dmax * dmax;
+    while (std::sqrt(hi) < dmax) hi = std::nextafter(hi, INFINITY);
+    while (std::sqrt(std::nextafter(hi, 0.0)) >= dmax) hi = std::nextafter(hi, 0.0);
+    P.scen_d2lo = lo;
+    P.scen_d2hi = hi;
+  }
   P.cos_pi6 = cos(pi / 6);
   for (int k = 0; k < 50; ++k) {
     const double ph = k * ((2 * pi - 0) / 50);   // np.linspace(0, 2pi, 50, endpoint=False)
@@ -4463,6 +4478,7 @@ int lsm_host_scenario(const lsm_config* cfg, const lsm_curriculum* cur, uint32_t
   sp.goal_speed_max = di ? 0.5 : 110 * 0.514444 * 0.001;
   sp.ratio_airtaxi = cur->ratio_airtaxi; sp.ratio_scenario = cur->ratio_scenario;
   sp.pi = 3.141592653589793; sp.two_pi = 2 * sp.pi;
+  sp.d2lo = sp.d2hi = 0.0;   // (the device draw's squared band; random_scenario tests d itself)
   std::vector<double> st(4 * N), lm(4 * NL), ws(SCEN_WS);
   if (cfg->rng == LSM_RNG_PHILOX) {   // the device's first reset (reset index 0) of this seed
     Philox m;

@@ -24,6 +24,7 @@ struct ScenarioParams {
   double ratio_airtaxi;     // curriculum_ratio_airtaxi in random_scenario
   double ratio_scenario;    // curriculum_ratio (1 with the filter, else sloped)
   double two_pi, pi;
+  double d2lo, d2hi;        // the device draw's band on squared distances (KParams::scen_d2lo / hi)
 };
 
 template <class Rng>

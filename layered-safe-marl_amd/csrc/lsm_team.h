@@ -83,16 +83,17 @@ __host__ __device__ inline size_t team_env_bytes(size_t bytes, int N) {
 
 // The next MT19937 block (HostMT::gen's arithmetic) into nxt, leaving key intact. Cooperative over
 // the env's 64 lanes: element i >= 227 reads nxt[i - 227], so chunks of 64 run in order.
+// Element i >= 227 reads nxt[i - 227], so three rounds: [0, 227) from the key, [227, 454) from the
+// first, [454, 624) from the second (the last element also reads nxt[0]).
 __device__ __forceinline__ void mt_next_block(const uint32_t* key, uint32_t* nxt) {
   const int lane = threadIdx.x & 63;
-  for (int i = lane; i < MT_N - MT_M; i += 64) nxt[i] = mt_twist1(key[i], key[i + 1], key[i + MT_M]);
+  constexpr int D = MT_N - MT_M;   // 227
+  for (int i = lane; i < D; i += 64) nxt[i] = mt_twist1(key[i], key[i + 1], key[i + MT_M]);
   esync<64>();
-  for (int base = MT_N - MT_M; base < MT_N - 1; base += 64) {
-    const int i = base + lane;
-    if (i < MT_N - 1) nxt[i] = mt_twist1(key[i], key[i + 1], nxt[i - (MT_N - MT_M)]);
-    esync<64>();
-  }
-  if (lane == 0) nxt[MT_N - 1] = mt_twist1(key[MT_N - 1], nxt[0], nxt[MT_M - 1]);
+  for (int i = D + lane; i < 2 * D; i += 64) nxt[i] = mt_twist1(key[i], key[i + 1], nxt[i - D]);
+  esync<64>();
+  for (int i = 2 * D + lane; i < MT_N; i += 64)
+    nxt[i] = i < MT_N - 1 ? mt_twist1(key[i], key[i + 1], nxt[i - D]) : mt_twist1(key[MT_N - 1], nxt[0], nxt[MT_M - 1]);
   esync<64>();
 }
 
@@ -201,14 +202,14 @@ __device__ int random_scenario_wave2(const V& v, const ScenarioParams& p, double
   }
   c += per * N;
   DSTAMP(23);
-  double x0, x1, y0, y1, dmin, dmax;
+  // the separation band (dmin, dmax) = (0.25, 0.75) x coordination_range (DI), (0.5, 1) x (airtaxi),
+  // as squared-distance thresholds p.d2lo / p.d2hi (fill_params)
+  double x0, x1, y0, y1;
   if (p.dyn == 0) {
     x0 = -0.5 * wsz; x1 = 0.5 * wsz; y0 = -0.5 * wsz; y1 = 0.5 * wsz;
-    dmin = 0.25 * p.coordination_range; dmax = 0.75 * p.coordination_range;
   } else {
     const double yw = 0.1 * (1 - cra) + 0.5 * cra;
     x0 = 0.0; x1 = 0.75 * wsz; y0 = -yw * wsz; y1 = yw * wsz;
-    dmin = 0.5 * p.coordination_range; dmax = p.coordination_range;
   }
   // Agent blocks in stream order: [point 0: 4][tries: 4 (acc + 1)][keep: 4, agents i > 0]
   // [speeds: 6, DI][noise: 2]; only acc varies. (1) The chain of block starts: per agent, point 0
@@ -226,8 +227,10 @@ __device__ int random_scenario_wave2(const V& v, const ScenarioParams& p, double
     const double ax = raw_uniform<V>(r[0], r[1], x0, x1), ay = raw_uniform<V>(r[2], r[3], y0, y1);
     const double x = raw_uniform<V>(r[4], r[5], x0, x1), y = raw_uniform<V>(r[6], r[7], y0, y1);
     const double dx = ax - x, dy = ay - y;
-    const double d = sqrt(dx * dx + dy * dy);
-    return (d > dmin && d < dmax) || j == 999;   // the 1000th try is kept whatever it is
+    // d = sqrt(dx * dx + dy * dy) in (dmin, dmax), tested on the square (exact: the band's ends are
+    // the squared-distance thresholds of the correctly rounded sqrt, fill_params)
+    const double d2 = dx * dx + dy * dy;
+    return (d2 > p.d2lo && d2 < p.d2hi) || j == 999;   // the 1000th try is kept whatever it is
   };
   // the first accepted try >= j0 of the agent at cs, 64 tries per ballot (the rare long loops)
   auto first_from = [&](int cs, int j0) -> int {

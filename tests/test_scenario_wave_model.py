@@ -221,3 +221,40 @@ def test_raw_words_are_the_uniform_stream():
     r = np.random.RandomState(9)
     for k in range(0, 64, 2):
         assert uni(w, k, -3.0, 5.0) == r.uniform(-3.0, 5.0)
+
+
+def _sq_band(dmin, dmax):
+    """fill_params' squared-distance band (lsm_rollout.hip): the largest s with sqrt(s) <= dmin and
+    the smallest s with sqrt(s) >= dmax, for the correctly rounded sqrt."""
+    lo = dmin * dmin
+    while np.sqrt(lo) > dmin:
+        lo = np.nextafter(lo, 0.0)
+    while np.sqrt(np.nextafter(lo, np.inf)) <= dmin:
+        lo = np.nextafter(lo, np.inf)
+    hi = dmax * dmax
+    while np.sqrt(hi) < dmax:
+        hi = np.nextafter(hi, np.inf)
+    while np.sqrt(np.nextafter(hi, 0.0)) >= dmax:
+        hi = np.nextafter(hi, 0.0)
+    return lo, hi
+
+
+@pytest.mark.parametrize("cr,f0,f1", [(4.0, 0.25, 0.75), (3 * 1.60934, 0.5, 1.0)])
+def test_squared_band_equals_sqrt_band(cr, f0, f1):
+    """random_scenario_wave2 accepts a try on d2 = dx*dx + dy*dy in (d2lo, d2hi) instead of
+    sqrt(d2) in (dmin, dmax): the same decision for every double d2 (both band ends probed a few
+    hundred ulps either side, plus random squared distances of the draw's range)."""
+    dmin, dmax = f0 * cr, f1 * cr
+    lo, hi = _sq_band(dmin, dmax)
+    probes = []
+    for t in (lo, hi, dmin * dmin, dmax * dmax):
+        x = t
+        for _ in range(300):
+            x = np.nextafter(x, 0.0)
+        for _ in range(600):
+            probes.append(x)
+            x = np.nextafter(x, np.inf)
+    rng = np.random.default_rng(7)
+    probes = np.concatenate([np.array(probes), rng.uniform(0.0, 4 * dmax * dmax, 200000)])
+    d = np.sqrt(probes)
+    np.testing.assert_array_equal((d > dmin) & (d < dmax), (probes > lo) & (probes < hi))
