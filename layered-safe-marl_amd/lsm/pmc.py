@@ -98,6 +98,9 @@ def main():
         print(json.dumps({"kernel": a.kernel, "launches": len(us), "mean_us": statistics.fmean(us),
                           "p50_us": q(0.5), "p90_us": q(0.9), "max_us": srt[-1],
                           "slowest": [(i, round(v, 2)) for i, v in sorted(enumerate(us), key=lambda x: -x[1])[:4]],
+                          # the two launches after each of those (the steps right after an auto-reset)
+                          "after_slowest": [[(j, round(us[j], 2)) for j in (i + 1, i + 2) if j < len(us)]
+                                            for i, _ in sorted(enumerate(us), key=lambda x: -x[1])[:4]],
                           "note": "the slowest launches are the auto-reset steps (MT19937 scenario replay)"}))
         return
     if a.cmd == "stats":
